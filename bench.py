@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Headline benchmark: min-snap trajectories/sec (10-seg, order-7, 3-axis) at batch = 65k.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one solve of one batch of B = 65,536 synthetic trajectories (M = 10)
+per GPU (BASELINE.json configs[2] / SURVEY.md §8(d) config 3), inputs resident in
+HBM when the timed region starts, coefficients written to HBM.  Trajectories are
+independent, so N GPUs each solve their own shard (weak scaling, no data-path
+collective).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6   # MI355X FP64 vector spec peak (dense-KKT roof, reported beside)
+
+
+def algorithmic_bytes_per_traj(M: int, with_status: bool = True) -> int:
+    """input (M+1)*3*8 waypoints + M*8 times, output M*3*8*8 coefficients
+    (+ 4 B status).  M = 10: 264 + 80 + 1920 (+4) bytes."""
+    return (M + 1) * 3 * 8 + M * 8 + M * 24 * 8 + (4 if with_status else 0)
+
+
+def dense_flops_per_traj(M: int) -> float:
+    N = 14 * M + 2
+    return 2.0 / 3.0 * N ** 3 + 6.0 * N ** 2
+
+
+def load_traffic(workload_key: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_baseline(B: int, M: int, target_s: float):
+    """The CPU oracle (build's own fp64 dense-KKT restatement; the reference has no
+    solver) on a bounded sample of the same workload, timed on this host."""
+    from oracle import oracle as O
+    from trajectory_generator_ros2_amd import synthetic as S
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "1") or 1)
+    so, W, T = S.uniform_batch(min(B, 4096), M)
+    t0 = time.perf_counter()
+    O.solve_batch(so[:257], W[:256], T[:256], None, O.KKT_C4, threads)
+    pilot = max(time.perf_counter() - t0, 1e-6) / 256.0
+    n = int(min(B, max(256, target_s / pilot)))
+    so, W, T = S.uniform_batch(n, M)
+    t0 = time.perf_counter()
+    _, st = O.solve_batch(so, W, T, None, O.KKT_C4, threads)
+    el = time.perf_counter() - t0
+    assert (st == 0).all()
+    return {"value": n / el, "unit": "trajectories/s", "cores": threads, "kind": "port",
+            "sample": f"{n} trajectories of the config-3 workload (M={M}), oracle dense KKT "
+                      f"(LU, partial pivoting, fp64), {threads} OpenMP thread(s), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
+    ap.add_argument("--segments", type=int, default=10)
+    ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
+    ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="0: skip the CPU baseline")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from trajectory_generator_ros2_amd import METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver
+
+    B, M = args.batch, args.segments
+    dev = torch.cuda.current_device()
+    solver = Solver(dev, METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
+    # this rank's shard of the job: independent trajectories, seed offset by rank
+    _, W, T = S.uniform_batch(B, M, seed=S.SEED + rank)
+    dW = torch.from_numpy(W).to(dev)
+    dT = torch.from_numpy(T).to(dev)
+    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev)
+    dS = torch.empty((B,), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+
+    K = args.steps
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev0[k].record(stream)
+        step()
+        ev1[k].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    launch_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
+
+    # dense-KKT side line (the survey's literal formulation), same inputs, same GPU
+    dense = None
+    if args.dense_steps > 0 and args.method == "reduced" and M <= 10:
+        solver.set_method(METHOD_DENSE_KKT)
+        dC2 = torch.empty_like(dC)
+        solver.solve_uniform_device(B, M, dW, dT, dC2, dS, stream=sp)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.dense_steps):
+            solver.solve_uniform_device(B, M, dW, dT, dC2, dS, stream=sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        dms = e0.elapsed_time(e1) / args.dense_steps
+        diff = (dC2 - dC).abs().amax(dim=(1, 3)) / dC.abs().amax(dim=(1, 3)).clamp_min(1e-300)
+        gfl = dense_flops_per_traj(M) * B / (dms * 1e-3) / 1e12
+        dense = {"value": B / (dms * 1e-3) * world, "ms_per_step": dms,
+                 "fp64_tflops_algorithmic": gfl, "fp64_peak_tflops": FP64_PEAK_TFS,
+                 "max_rel_diff_vs_reduced": float(diff.max().item())}
+        solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(B, M, args.cpu_seconds)
+
+    if rank == 0:
+        bpl = algorithmic_bytes_per_traj(M) * B
+        achieved = bpl / (launch_ms * 1e-3) / 1e9
+        key = f"B{B}_M{M}_{args.method}"
+        traffic = load_traffic(key)
+        value = world * B * K / el
+        line = {
+            "metric": "min-snap trajectories/sec (10-seg, order-7, 3-axis) at batch=65k; 1/2/4/8 GPU",
+            "value": value,
+            "unit": "trajectories/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": el / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md 8(d): seed 20251015+rank, room-bound uniform waypoints, "
+                    "T=clip(|dw|/1m/s,0.5,10), rest-to-rest)",
+            "config": {"workload": f"config3: {B} trajectories/GPU x {M} segments, order 7, 3 axes, "
+                                   f"coefficients [traj][seg][axis][8] fp64 in HBM",
+                       "batch_per_gpu": B, "segments": M, "method": args.method,
+                       "parallelism": f"shard{world} (independent trajectories, no collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": f"k_reduced_uniform<{M}>" if args.method == "reduced" else f"k_dense_kkt<{M}>",
+                         "launch_ms": launch_ms,
+                         "algorithmic_bytes_per_launch": bpl},
+            "cpu_baseline": cpu,
+            "dense_kkt": dense,
+        }
+        print(json.dumps(line), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

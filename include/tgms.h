@@ -1,0 +1,132 @@
+/*
+ * tgms.h — C ABI of the MI355X-native batched minimum-snap solver (libtgms.so).
+ *
+ * This is the drop-in boundary of SURVEY.md §8(b).  The reference
+ * (jrached/trajectory_generator_ros2) owns trajectories through
+ *     std::unique_ptr<Trajectory> traj_           include/trajectory_generator_ros2/TrajectoryGenerator.hpp:83
+ * built by the traj_type factory                  src/TrajectoryGenerator.cpp:175-388
+ * and calls exactly three virtuals on it:
+ *     generateTraj(goals, index_msgs, clock)      Trajectory.hpp:33-35, called at src/TrajectoryGenerator.cpp:71
+ *     generateStopTraj(goals, msgs, idx, clock)   Trajectory.hpp:38-41, called at src/TrajectoryGenerator.cpp:516
+ *     trajectoryInsideBounds(xmin..zmax)          Trajectory.hpp:44-46, called at src/TrajectoryGenerator.cpp:419
+ * The reference has no solver behind those virtuals (every primitive is a
+ * closed-form sampler).  A MinSnap primitive implements them on top
+ * of the entry points below (trajectory_generator_ros2_amd/host/MinSnap.cpp):
+ *     generateTraj            -> tgms_solve_batch (B = 1)  + tgms_sample_batch
+ *     generateStopTraj        -> tgms_solve_batch with end_derivs (braking)  + tgms_sample_batch
+ *     trajectoryInsideBounds  -> host check of waypoints and sampled extrema
+ * and a swarm / sampling planner calls the same entry points with B up to 10^6.
+ *
+ * Conventions:
+ *   - plain C, no exceptions cross the ABI; every call returns a tgms_status;
+ *   - the caller owns every I/O buffer; the handle owns device workspace only;
+ *   - a handle is bound to one HIP device and is single-thread-affine (the
+ *     reference calls from its single rclcpp executor thread,
+ *     src/trajectory_generator_node.cpp:30);
+ *   - `*_device` entry points take device pointers and a hipStream_t passed as
+ *     void* and are asynchronous; the others take host pointers and block;
+ *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
+ *     TGMS_ERR_NO_DEVICE.
+ *
+ * Layouts (fp64, row-major, trajectory-major).  A batch is CSR over segments:
+ * trajectory b has M_b = seg_offsets[b+1] - seg_offsets[b] segments (1..TGMS_MAX_SEGMENTS):
+ *   seg_offsets  int32 [B+1], seg_offsets[0] = 0, non-decreasing
+ *   waypoints    [sum_b (M_b+1)][3]   rows of b start at seg_offsets[b] + b
+ *   seg_times    [sum_b M_b]          T_i > 0 and finite, starting at seg_offsets[b]
+ *   end_derivs   NULL (rest-to-rest, as every reference primitive starts and ends
+ *                at rest) or [B][2][3][3] = [start|final][v,a,j][x,y,z]
+ *   coeffs       [sum_b M_b][3][8]    p(t) = sum_j c_j t^j on local t in [0, T_i]
+ *   status       int32 [B], nullable: per-trajectory tgms_status
+ */
+#ifndef TGMS_H
+#define TGMS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGMS_ABI_VERSION 1
+#define TGMS_MAX_SEGMENTS 16       /* reduced-Hessian kernel: M = 1..16 (config 5 range) */
+#define TGMS_DENSE_MAX_SEGMENTS 10 /* dense KKT kernel: N = 14M+2 <= 142 fits 160 KiB LDS */
+#define TGMS_GOAL_STRIDE 14        /* doubles per sample: p[3] v[3] a[3] j[3] psi dpsi */
+
+typedef enum tgms_status {
+    TGMS_OK = 0,
+    TGMS_ERR_INVALID_ARG = 1, /* bad sizes/pointers, M_b < 1 or > max, T <= 0, non-finite input */
+    TGMS_ERR_SINGULAR = 2,    /* a pivot / Cholesky block broke down */
+    TGMS_ERR_NONFINITE = 3,   /* solution contains inf/nan */
+    TGMS_ERR_NO_DEVICE = 4,   /* no HIP device (no CPU fallback exists) */
+    TGMS_ERR_DEVICE = 5,      /* a HIP runtime call failed (see tgms_last_error) */
+    TGMS_ERR_UNSUPPORTED = 6  /* e.g. dense-KKT method with M_b > TGMS_DENSE_MAX_SEGMENTS */
+} tgms_status;
+
+typedef enum tgms_method {
+    TGMS_METHOD_REDUCED = 0,  /* default: Schur complement of the KKT onto the free knot
+                                 derivatives, block-tridiagonal LDL^T, one lane per trajectory */
+    TGMS_METHOD_DENSE_KKT = 1 /* the survey's literal a1-a3: KKT assembled in LDS, partial-
+                                 pivoting LU, one wavefront per trajectory */
+} tgms_method;
+
+typedef enum tgms_yaw_mode {
+    TGMS_YAW_CONSTANT = 0, /* psi = yaw_const, dpsi = 0 */
+    TGMS_YAW_VELOCITY = 1  /* psi = atan2(v_y, v_x) (Figure8.cpp:123 convention) when
+                              |v_xy| > 1e-3, else yaw_const; dpsi = d/dt psi */
+} tgms_yaw_mode;
+
+typedef struct tgms_handle tgms_handle;
+
+int tgms_abi_version(void);
+const char* tgms_status_string(int status);
+
+/* Create a handle on HIP device `device` (ordinal).  TGMS_ERR_NO_DEVICE if none. */
+tgms_status tgms_create(tgms_handle** out, int device);
+void tgms_destroy(tgms_handle* h);
+/* Last error text of this handle ("" if none).  Valid until the next call. */
+const char* tgms_last_error(const tgms_handle* h);
+tgms_status tgms_set_method(tgms_handle* h, int method);
+
+/* ---- solve (host pointers, blocking) ---- */
+tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* seg_offsets,
+                             const double* waypoints, const double* seg_times,
+                             const double* end_derivs, double* coeffs, int32_t* status);
+
+/* ---- solve (device pointers, asynchronous on `stream`) ---- */
+/* Uniform batch: every trajectory has M segments (configs 2-4). */
+tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M,
+                                      const double* d_waypoints, const double* d_seg_times,
+                                      const double* d_end_derivs, double* d_coeffs,
+                                      int32_t* d_status, void* stream);
+/* Ragged batch (config 5).  h_seg_offsets is a host copy used to plan the launch
+ * (trajectories are grouped by M so every wavefront runs one M). */
+tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
+                                    const int32_t* d_seg_offsets, const double* d_waypoints,
+                                    const double* d_seg_times, const double* d_end_derivs,
+                                    double* d_coeffs, int32_t* d_status, void* stream);
+
+/* ---- sampling at dt ----
+ * Trajectory b yields tgms_sample_count(sum_i T_i, dt) samples: t_k = k*dt for
+ * k = 0 .. n-2 and a final sample at sum_i T_i pinned exactly to the last
+ * waypoint and final end derivatives (the Line.cpp:80-82 convention).  Each sample
+ * is TGMS_GOAL_STRIDE doubles.  sample_offsets [B+1] comes from
+ * tgms_sample_offsets(). */
+int64_t tgms_sample_count(double total_T, double dt);
+tgms_status tgms_sample_offsets(int32_t B, const int32_t* seg_offsets, const double* seg_times,
+                                double dt, int64_t* sample_offsets);
+tgms_status tgms_sample_batch(tgms_handle* h, int32_t B, const int32_t* seg_offsets,
+                              const double* waypoints, const double* seg_times,
+                              const double* end_derivs, const double* coeffs, double dt,
+                              int yaw_mode, double yaw_const, const int64_t* sample_offsets,
+                              double* out);
+tgms_status tgms_sample_batch_device(tgms_handle* h, int32_t B, const int32_t* d_seg_offsets,
+                                     const double* d_waypoints, const double* d_seg_times,
+                                     const double* d_end_derivs, const double* d_coeffs,
+                                     double dt, int yaw_mode, double yaw_const,
+                                     const int64_t* d_sample_offsets, double* d_out,
+                                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TGMS_H */

@@ -1,0 +1,223 @@
+"""GPU parity: libtgms (HIP, gfx950) through its C ABI vs the oracle and the exact goldens.
+
+Tolerance (BASELINE.json north_star): per (trajectory, axis),
+norm-wise  ||c_gpu - c_ref||_inf / ||c_ref||_inf <= 1e-9.  Element-wise relative
+error is not used: rest-to-rest segments have exact zero coefficients.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import batch_rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _uniform(B, M, seed):
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(B, M, seed=seed)
+    return so, W.reshape(-1, 3), T.reshape(-1)
+
+
+def _methods():
+    from trajectory_generator_ros2_amd import METHOD_DENSE_KKT, METHOD_REDUCED
+    return [METHOD_REDUCED, METHOD_DENSE_KKT]
+
+
+@pytest.mark.parametrize("M", list(range(1, 17)))
+def test_reduced_uniform_vs_oracle(solver, oracle, M):
+    so, W, T = _uniform(257, M, seed=100 + M)  # 257: last wavefront partially filled
+    C, st, worst = solver.solve(so, W, T)
+    assert worst == 0 and (st == 0).all()
+    R, rst = oracle.solve_batch(so, W, T, None, oracle.KKT_C4 if M <= 10 else oracle.REDUCED)
+    assert (rst == 0).all()
+    assert batch_rel_err(so, C, R) <= TOL
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 10])
+def test_dense_kkt_uniform_vs_oracle(solver, oracle, M):
+    from trajectory_generator_ros2_amd import METHOD_DENSE_KKT, METHOD_REDUCED
+    so, W, T = _uniform(130, M, seed=200 + M)
+    solver.set_method(METHOD_DENSE_KKT)
+    try:
+        C, st, worst = solver.solve(so, W, T)
+    finally:
+        solver.set_method(METHOD_REDUCED)
+    assert worst == 0 and (st == 0).all()
+    R, _ = oracle.solve_batch(so, W, T, None, oracle.KKT_C4)
+    assert batch_rel_err(so, C, R) <= TOL
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_end_derivs_vs_oracle(solver, oracle, method):
+    rng = np.random.default_rng(5)
+    M = 6 if method == 1 else 9
+    so, W, T = _uniform(200, M, seed=300)
+    ED = rng.normal(size=(200, 18))
+    solver.set_method(method)
+    try:
+        C, st, worst = solver.solve(so, W, T, ED)
+    finally:
+        solver.set_method(0)
+    assert worst == 0
+    R, _ = oracle.solve_batch(so, W, T, ED, oracle.KKT_C4)
+    assert batch_rel_err(so, C, R) <= TOL
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_ragged_vs_oracle(solver, oracle, method):
+    from trajectory_generator_ros2_amd import synthetic as S
+    hi = 16 if method == 0 else 10
+    so, W, T = S.ragged_batch(1000, 1, hi, seed=400 + method)
+    solver.set_method(method)
+    try:
+        C, st, worst = solver.solve(so, W, T)
+    finally:
+        solver.set_method(0)
+    assert worst == 0 and (st == 0).all()
+    R, _ = oracle.solve_batch(so, W, T, None, oracle.REDUCED)
+    assert batch_rel_err(so, C, R) <= TOL
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))))
+@pytest.mark.parametrize("method", [0, 1])
+def test_goldens_exact(solver, path, method):
+    g = np.load(path)
+    so = g["seg_offsets"]
+    if method == 1 and int(np.diff(so).max()) > 10:
+        pytest.skip("dense KKT supports M <= 10")
+    ED = g["end_derivs"] if "end_derivs" in g.files else None
+    solver.set_method(method)
+    try:
+        C, st, worst = solver.solve(so, g["waypoints"], g["seg_times"], ED)
+    finally:
+        solver.set_method(0)
+    assert worst == 0
+    assert batch_rel_err(so, C, g["coeffs"]) <= TOL
+
+
+def test_invalid_inputs(solver):
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_UNSUPPORTED
+    so, W, T = _uniform(70, 4, seed=7)
+    T = T.copy(); W = W.copy()
+    T[4 * 3 + 1] = 0.0        # trajectory 3: T <= 0
+    T[4 * 5] = -1.0           # trajectory 5
+    W[(4 + 1) * 9 + 2, 1] = np.nan  # trajectory 9: NaN waypoint
+    T[4 * 66 + 3] = np.inf    # trajectory 66 (second wavefront)
+    for method in (0, 1):
+        solver.set_method(method)
+        C, st, worst = solver.solve(so, W, T)
+        bad = {3, 5, 9, 66}
+        assert worst == ERR_INVALID_ARG
+        assert all(st[b] == ERR_INVALID_ARG for b in bad)
+        assert all(st[b] == 0 for b in range(70) if b not in bad)
+        assert np.isfinite(C).all()
+    solver.set_method(0)
+    # structural errors are reported by the host before any launch
+    _, _, w = solver.solve(np.array([0, 0], np.int32), np.zeros((1, 3)), np.zeros(0))
+    assert w == ERR_INVALID_ARG
+    so17, W17, T17 = _uniform(2, 17, seed=1)
+    assert solver.solve(so17, W17, T17)[2] == ERR_INVALID_ARG
+    so11, W11, T11 = _uniform(2, 11, seed=1)
+    solver.set_method(1)
+    assert solver.solve(so11, W11, T11)[2] == ERR_UNSUPPORTED
+    solver.set_method(0)
+
+
+def test_config3_full_size_properties(solver, oracle):
+    """BASELINE config 3 at full size (B = 65,536, M = 10) through the device API:
+    parity with the oracle on every trajectory + size-independent properties."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    B, M = 65536, 10
+    so, W, T = S.uniform_batch(B, M)
+    dW = torch.from_numpy(W).cuda()
+    dT = torch.from_numpy(T).cuda()
+    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+    dS = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    C = dC.cpu().numpy().reshape(-1, 3, 8)
+    assert (dS.cpu().numpy() == 0).all()
+    R, _ = oracle.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, oracle.REDUCED)
+    assert batch_rel_err(so, C, R) <= TOL
+    # interpolation and C6 continuity at every interior knot, rest at both ends
+    Cb = C.reshape(B, M, 3, 8)
+    j = np.arange(8)
+    Tt = T.reshape(B, M, 1, 1)
+
+    def deriv(c, t, k):
+        f = np.array([np.prod(np.arange(jj - k + 1, jj + 1)) if jj >= k else 0.0 for jj in j])
+        p = np.where(j >= k, j - k, 0)
+        return (c * f * np.power(t, p)).sum(-1)
+
+    np.testing.assert_allclose(Cb[..., 0], W[:, :-1, :], rtol=0, atol=1e-12)
+    end_p = deriv(Cb, Tt, 0)
+    np.testing.assert_allclose(end_p, W[:, 1:, :], rtol=0, atol=1e-8)
+    for k in range(1, 7):
+        left = deriv(Cb[:, :-1], Tt[:, :-1], k)
+        right = deriv(Cb[:, 1:], 0.0 * Tt[:, 1:], k)
+        scale = np.abs(right).max() + 1.0
+        assert np.abs(left - right).max() <= 1e-7 * scale, k
+    for k in range(1, 4):
+        assert np.abs(Cb[:, 0, :, k]).max() == 0.0
+        assert np.abs(deriv(Cb[:, -1], Tt[:, -1], k)).max() <= 1e-8
+
+
+def test_device_ragged_matches_host(solver):
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(5000, 2, 16, seed=9)
+    C_host, st, worst = solver.solve(so, W, T)
+    assert worst == 0
+    dso = torch.from_numpy(so).cuda()
+    dC = torch.zeros((int(so[-1]), 3, 8), dtype=torch.float64, device="cuda")
+    solver.solve_batch_device(so, dso, torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda(), dC,
+                              stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(dC.cpu().numpy(), C_host)
+
+
+def test_sampler_vs_oracle(solver, oracle):
+    from trajectory_generator_ros2_amd import YAW_VELOCITY
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(40, 1, 16, seed=12)
+    C, _, worst = solver.solve(so, W, T)
+    assert worst == 0
+    for yaw_mode in (0, YAW_VELOCITY):
+        offs, out = solver.sample(so, W, T, None, C, 0.01, yaw_mode, 0.3)
+        for b in range(40):
+            s0, s1 = so[b], so[b + 1]
+            ref = oracle.sample(C[s0:s1], T[s0:s1], W[s0 + b:s1 + b + 1], None, 0.01, yaw_mode, 0.3)
+            got = out[offs[b]:offs[b + 1]]
+            assert got.shape == ref.shape
+            for f0, f1 in ((0, 3), (3, 6), (6, 9), (9, 12)):
+                scale = max(np.abs(ref[:, f0:f1]).max(), 1e-300)
+                assert np.abs(got[:, f0:f1] - ref[:, f0:f1]).max() <= TOL * scale
+            assert np.array_equal(got[-1, :12], ref[-1, :12])  # pinned final sample
+            sp = np.hypot(ref[:, 3], ref[:, 4])
+            m = (sp > 2e-3)
+            dpsi = np.angle(np.exp(1j * (got[m, 12] - ref[m, 12])))
+            assert np.abs(dpsi).max() <= 1e-9
+            m0 = (sp < 5e-4)
+            assert np.array_equal(got[m0, 12], ref[m0, 12])
+
+
+@pytest.mark.parametrize("name", ["c1", "c3_sampled", "end_derivs"])
+def test_sampler_vs_exact_golden(solver, name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    so = g["seg_offsets"]
+    ED = g["end_derivs"] if "end_derivs" in g.files else None
+    C, _, worst = solver.solve(so, g["waypoints"], g["seg_times"], ED)
+    assert worst == 0
+    offs, out = solver.sample(so, g["waypoints"], g["seg_times"], ED, C, float(g["dt"]))
+    assert np.array_equal(offs, g["sample_offsets"])
+    ref = g["samples"]
+    for f0, f1 in ((0, 3), (3, 6), (6, 9), (9, 12)):
+        scale = np.abs(ref[:, f0:f1]).max()
+        assert np.abs(out[:, f0:f1] - ref[:, f0:f1]).max() <= TOL * scale

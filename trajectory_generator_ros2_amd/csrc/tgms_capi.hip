@@ -1,0 +1,396 @@
+// tgms_capi.hip — C ABI of libtgms (include/tgms.h): handles, validation,
+// host<->device staging, ragged-batch planning and kernel dispatch.
+//
+// Error conventions mirror the reference's boundary: no C++
+// exceptions cross the ABI, every entry point returns a tgms_status, and the
+// MinSnap adapter maps a failure to the reference's RCLCPP_ERROR + exit(1)
+// (Line.cpp:77-78).  There is deliberately NO CPU fallback: without a HIP
+// device tgms_create() fails with TGMS_ERR_NO_DEVICE.
+#include "tgms.h"
+#include "tgms_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+struct tgms_handle {
+    int device = 0;
+    int method = TGMS_METHOD_REDUCED;
+    hipStream_t stream = nullptr;  // stream of the blocking (host-pointer) API
+    std::string last_error;
+    // grow-only device workspace for the host-pointer API and ragged plans
+    void* d_ws = nullptr;
+    size_t ws_cap = 0;
+    int32_t* d_perm = nullptr;  // ragged plan: trajectory ids grouped by M
+    size_t perm_cap = 0;
+    int32_t* h_perm = nullptr;  // pinned staging of the plan
+    size_t h_perm_cap = 0;
+    hipEvent_t perm_ev = nullptr;  // guards h_perm reuse until the upload completed
+};
+
+namespace {
+
+tgms_status set_err(tgms_handle* h, tgms_status st, const std::string& msg) {
+    if (h) h->last_error = msg;
+    return st;
+}
+
+tgms_status hip_err(tgms_handle* h, hipError_t e, const char* where) {
+    if (e == hipSuccess) return TGMS_OK;
+    return set_err(h, TGMS_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define TGMS_HIP(h, call)                                  \
+    do {                                                   \
+        hipError_t e_ = (call);                            \
+        if (e_ != hipSuccess) return hip_err(h, e_, #call); \
+    } while (0)
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+tgms_status ensure_ws(tgms_handle* h, size_t bytes) {
+    if (bytes <= h->ws_cap) return TGMS_OK;
+    if (h->d_ws) {
+        TGMS_HIP(h, hipStreamSynchronize(h->stream));
+        TGMS_HIP(h, hipFree(h->d_ws));
+        h->d_ws = nullptr;
+        h->ws_cap = 0;
+    }
+    TGMS_HIP(h, hipMalloc(&h->d_ws, bytes));
+    h->ws_cap = bytes;
+    return TGMS_OK;
+}
+
+// Validates a CSR segment layout on the host; fills per-M counts.
+tgms_status check_offsets(tgms_handle* h, int32_t B, const int32_t* so, int max_m,
+                          std::vector<int32_t>* counts, int* uniform_m) {
+    if (B < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "B < 0");
+    if (!so) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets is NULL");
+    if (so[0] != 0) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets[0] != 0");
+    if (counts) counts->assign(max_m + 1, 0);
+    int um = -1;
+    for (int32_t b = 0; b < B; ++b) {
+        const int32_t M = so[b + 1] - so[b];
+        if (M < 1 || M > TGMS_MAX_SEGMENTS) {
+            char buf[128];
+            snprintf(buf, sizeof buf, "trajectory %d has %d segments (allowed 1..%d)", b, M,
+                     TGMS_MAX_SEGMENTS);
+            return set_err(h, TGMS_ERR_INVALID_ARG, buf);
+        }
+        if (M > max_m) {
+            char buf[128];
+            snprintf(buf, sizeof buf, "trajectory %d has %d segments; method supports <= %d", b, M, max_m);
+            return set_err(h, TGMS_ERR_UNSUPPORTED, buf);
+        }
+        if (counts) (*counts)[M]++;
+        um = (b == 0) ? M : (um == M ? M : 0);
+    }
+    if (uniform_m) *uniform_m = um;
+    return TGMS_OK;
+}
+
+// Groups trajectories by M (counting sort) and uploads the permutation.
+tgms_status upload_plan(tgms_handle* h, int32_t B, const int32_t* so,
+                        const std::vector<int32_t>& counts, std::vector<int32_t>* starts,
+                        hipStream_t stream) {
+    starts->assign(counts.size() + 1, 0);
+    for (size_t m = 1; m < counts.size(); ++m) (*starts)[m + 1] = (*starts)[m] + counts[m];
+    if ((size_t)B > h->h_perm_cap) {
+        if (h->h_perm) {
+            TGMS_HIP(h, hipEventSynchronize(h->perm_ev));
+            TGMS_HIP(h, hipHostFree(h->h_perm));
+        }
+        TGMS_HIP(h, hipHostMalloc(reinterpret_cast<void**>(&h->h_perm), sizeof(int32_t) * B));
+        h->h_perm_cap = B;
+    }
+    if ((size_t)B > h->perm_cap) {
+        if (h->d_perm) {
+            TGMS_HIP(h, hipDeviceSynchronize());
+            TGMS_HIP(h, hipFree(h->d_perm));
+        }
+        TGMS_HIP(h, hipMalloc(reinterpret_cast<void**>(&h->d_perm), sizeof(int32_t) * B));
+        h->perm_cap = B;
+    }
+    TGMS_HIP(h, hipEventSynchronize(h->perm_ev));  // previous upload must have drained
+    std::vector<int32_t> fill(starts->begin(), starts->end());
+    for (int32_t b = 0; b < B; ++b) h->h_perm[fill[so[b + 1] - so[b]]++] = b;
+    TGMS_HIP(h, hipMemcpyAsync(h->d_perm, h->h_perm, sizeof(int32_t) * B, hipMemcpyHostToDevice, stream));
+    TGMS_HIP(h, hipEventRecord(h->perm_ev, stream));
+    return TGMS_OK;
+}
+
+tgms_status dispatch(tgms_handle* h, int32_t B, int uniform_m, const std::vector<int32_t>& counts,
+                     const int32_t* h_so, const int32_t* d_so, const double* W, const double* T,
+                     const double* ED, double* C, int32_t* st, hipStream_t stream) {
+    if (B == 0) return TGMS_OK;
+    if (h->method == TGMS_METHOD_REDUCED && uniform_m > 0) {
+        TGMS_HIP(h, tgms::launch_reduced_uniform(uniform_m, B, W, T, ED, C, st, stream));
+        return TGMS_OK;
+    }
+    if (h->method == TGMS_METHOD_DENSE_KKT && uniform_m > 0) {
+        TGMS_HIP(h, tgms::launch_dense_kkt(uniform_m, B, nullptr, nullptr, W, T, ED, C, st, stream));
+        return TGMS_OK;
+    }
+    std::vector<int32_t> starts;
+    tgms_status s = upload_plan(h, B, h_so, counts, &starts, stream);
+    if (s != TGMS_OK) return s;
+    for (size_t m = 1; m < counts.size(); ++m) {
+        if (!counts[m]) continue;
+        const int32_t* ids = h->d_perm + starts[m];
+        if (h->method == TGMS_METHOD_REDUCED)
+            TGMS_HIP(h, tgms::launch_reduced_ragged_group((int)m, counts[m], ids, d_so, W, T, ED, C, st, stream));
+        else
+            TGMS_HIP(h, tgms::launch_dense_kkt((int)m, counts[m], ids, d_so, W, T, ED, C, st, stream));
+    }
+    return TGMS_OK;
+}
+
+int max_m_for(const tgms_handle* h) {
+    return h->method == TGMS_METHOD_DENSE_KKT ? TGMS_DENSE_MAX_SEGMENTS : TGMS_MAX_SEGMENTS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgms_abi_version(void) { return TGMS_ABI_VERSION; }
+
+const char* tgms_status_string(int status) {
+    switch (status) {
+        case TGMS_OK: return "TGMS_OK";
+        case TGMS_ERR_INVALID_ARG: return "TGMS_ERR_INVALID_ARG";
+        case TGMS_ERR_SINGULAR: return "TGMS_ERR_SINGULAR";
+        case TGMS_ERR_NONFINITE: return "TGMS_ERR_NONFINITE";
+        case TGMS_ERR_NO_DEVICE: return "TGMS_ERR_NO_DEVICE";
+        case TGMS_ERR_DEVICE: return "TGMS_ERR_DEVICE";
+        case TGMS_ERR_UNSUPPORTED: return "TGMS_ERR_UNSUPPORTED";
+        default: return "TGMS_ERR_UNKNOWN";
+    }
+}
+
+tgms_status tgms_create(tgms_handle** out, int device) {
+    if (!out) return TGMS_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return TGMS_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return TGMS_ERR_INVALID_ARG;
+    tgms_handle* h = new tgms_handle();
+    h->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->perm_ev, hipEventDisableTiming) != hipSuccess) {
+        delete h;
+        return TGMS_ERR_DEVICE;
+    }
+    *out = h;
+    return TGMS_OK;
+}
+
+void tgms_destroy(tgms_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();
+    if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->d_perm) (void)hipFree(h->d_perm);
+    if (h->h_perm) (void)hipHostFree(h->h_perm);
+    if (h->perm_ev) (void)hipEventDestroy(h->perm_ev);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char* tgms_last_error(const tgms_handle* h) { return h ? h->last_error.c_str() : ""; }
+
+tgms_status tgms_set_method(tgms_handle* h, int method) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "unknown method");
+    h->method = method;
+    return TGMS_OK;
+}
+
+tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,
+                             const double* seg_times, const double* end_derivs, double* coeffs,
+                             int32_t* status) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    std::vector<int32_t> counts;
+    int um = 0;
+    tgms_status s = check_offsets(h, B, so, max_m_for(h), &counts, &um);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!waypoints || !seg_times || !coeffs)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times/coeffs");
+    TGMS_HIP(h, hipSetDevice(h->device));
+    const size_t S = (size_t)so[B];
+    const size_t nW = (S + B) * 3, nT = S, nED = end_derivs ? (size_t)B * 18 : 0, nC = S * 24;
+    size_t off = 0;
+    const size_t oW = off; off = align256(off + nW * 8);
+    const size_t oT = off; off = align256(off + nT * 8);
+    const size_t oED = off; off = align256(off + nED * 8);
+    const size_t oC = off; off = align256(off + nC * 8);
+    const size_t oSt = off; off = align256(off + (size_t)B * 4);
+    const size_t oSo = off; off = align256(off + (size_t)(B + 1) * 4);
+    s = ensure_ws(h, off);
+    if (s != TGMS_OK) return s;
+    char* base = static_cast<char*>(h->d_ws);
+    double* dW = reinterpret_cast<double*>(base + oW);
+    double* dT = reinterpret_cast<double*>(base + oT);
+    double* dED = end_derivs ? reinterpret_cast<double*>(base + oED) : nullptr;
+    double* dC = reinterpret_cast<double*>(base + oC);
+    int32_t* dSt = reinterpret_cast<int32_t*>(base + oSt);
+    int32_t* dSo = reinterpret_cast<int32_t*>(base + oSo);
+    hipStream_t st = h->stream;
+    TGMS_HIP(h, hipMemcpyAsync(dW, waypoints, nW * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dT, seg_times, nT * 8, hipMemcpyHostToDevice, st));
+    if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    s = dispatch(h, B, um, counts, so, dSo, dW, dT, dED, dC, dSt, st);
+    if (s != TGMS_OK) return s;
+    TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> hst;
+    int32_t* stout = status;
+    if (!stout) {
+        hst.resize(B);
+        stout = hst.data();
+    }
+    TGMS_HIP(h, hipMemcpyAsync(stout, dSt, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    TGMS_HIP(h, hipStreamSynchronize(st));
+    int worst = TGMS_OK;
+    for (int32_t b = 0; b < B; ++b) worst = std::max(worst, (int)stout[b]);
+    if (worst != TGMS_OK) {
+        for (int32_t b = 0; b < B; ++b)
+            if (stout[b] == worst) {
+                char buf[160];
+                snprintf(buf, sizeof buf, "trajectory %d: %s", b, tgms_status_string(worst));
+                h->last_error = buf;
+                break;
+            }
+    }
+    return (tgms_status)worst;
+}
+
+tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* dW,
+                                      const double* dT, const double* dED, double* dC,
+                                      int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    if (B < 0 || M < 1 || M > max_m_for(h))
+        return set_err(h, M > TGMS_MAX_SEGMENTS || M < 1 || B < 0 ? TGMS_ERR_INVALID_ARG : TGMS_ERR_UNSUPPORTED,
+                       "bad B or M for this method");
+    if (B == 0) return TGMS_OK;
+    if (!dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (h->method == TGMS_METHOD_REDUCED)
+        TGMS_HIP(h, tgms::launch_reduced_uniform(M, B, dW, dT, dED, dC, dSt, st));
+    else
+        TGMS_HIP(h, tgms::launch_dense_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, st));
+    return TGMS_OK;
+}
+
+tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_so,
+                                    const int32_t* d_so, const double* dW, const double* dT,
+                                    const double* dED, double* dC, int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    std::vector<int32_t> counts;
+    int um = 0;
+    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), &counts, &um);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    return dispatch(h, B, um, counts, h_so, d_so, dW, dT, dED, dC, dSt, static_cast<hipStream_t>(stream));
+}
+
+int64_t tgms_sample_count(double total_T, double dt) {
+    if (!(dt > 0.0) || !(total_T >= 0.0) || !std::isfinite(total_T)) return 0;
+    const double x = std::ceil(total_T / dt - 1e-9);
+    int64_t n = (int64_t)x;
+    if (n < 1) n = 1;
+    return n + 1;
+}
+
+tgms_status tgms_sample_offsets(int32_t B, const int32_t* so, const double* T, double dt,
+                                int64_t* sample_offsets) {
+    if (B < 0 || !so || !sample_offsets || (B > 0 && !T) || !(dt > 0.0)) return TGMS_ERR_INVALID_ARG;
+    sample_offsets[0] = 0;
+    for (int32_t b = 0; b < B; ++b) {
+        double tot = 0.0;
+        for (int32_t i = so[b]; i < so[b + 1]; ++i) tot += T[i];
+        const int64_t n = tgms_sample_count(tot, dt);
+        if (n <= 0) return TGMS_ERR_INVALID_ARG;
+        sample_offsets[b + 1] = sample_offsets[b] + n;
+    }
+    return TGMS_OK;
+}
+
+tgms_status tgms_sample_batch_device(tgms_handle* h, int32_t B, const int32_t* d_so,
+                                     const double* dW, const double* dT, const double* dED,
+                                     const double* dC, double dt, int yaw_mode, double yaw_const,
+                                     const int64_t* d_sample_offsets, double* d_out, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    if (B < 0 || !(dt > 0.0) || (yaw_mode != TGMS_YAW_CONSTANT && yaw_mode != TGMS_YAW_VELOCITY))
+        return set_err(h, TGMS_ERR_INVALID_ARG, "bad B, dt or yaw_mode");
+    if (B == 0) return TGMS_OK;
+    if (!d_so || !dW || !dT || !dC || !d_sample_offsets || !d_out)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_HIP(h, tgms::launch_sample(B, d_so, dW, dT, dED, dC, dt, yaw_mode, yaw_const, d_sample_offsets,
+                                    d_out, static_cast<hipStream_t>(stream)));
+    return TGMS_OK;
+}
+
+tgms_status tgms_sample_batch(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,
+                              const double* seg_times, const double* end_derivs, const double* coeffs,
+                              double dt, int yaw_mode, double yaw_const,
+                              const int64_t* sample_offsets, double* out) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    tgms_status s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!waypoints || !seg_times || !coeffs || !sample_offsets || !out || !(dt > 0.0))
+        return set_err(h, TGMS_ERR_INVALID_ARG, "NULL pointer or dt <= 0");
+    if (yaw_mode != TGMS_YAW_CONSTANT && yaw_mode != TGMS_YAW_VELOCITY)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "bad yaw_mode");
+    TGMS_HIP(h, hipSetDevice(h->device));
+    const size_t S = (size_t)so[B];
+    const size_t nS = (size_t)sample_offsets[B];
+    const size_t nW = (S + B) * 3, nT = S, nED = end_derivs ? (size_t)B * 18 : 0, nC = S * 24;
+    size_t off = 0;
+    const size_t oW = off; off = align256(off + nW * 8);
+    const size_t oT = off; off = align256(off + nT * 8);
+    const size_t oED = off; off = align256(off + nED * 8);
+    const size_t oC = off; off = align256(off + nC * 8);
+    const size_t oSo = off; off = align256(off + (size_t)(B + 1) * 4);
+    const size_t oSmp = off; off = align256(off + (size_t)(B + 1) * 8);
+    const size_t oOut = off; off = align256(off + nS * TGMS_GOAL_STRIDE * 8);
+    s = ensure_ws(h, off);
+    if (s != TGMS_OK) return s;
+    char* base = static_cast<char*>(h->d_ws);
+    double* dW = reinterpret_cast<double*>(base + oW);
+    double* dT = reinterpret_cast<double*>(base + oT);
+    double* dED = end_derivs ? reinterpret_cast<double*>(base + oED) : nullptr;
+    double* dC = reinterpret_cast<double*>(base + oC);
+    int32_t* dSo = reinterpret_cast<int32_t*>(base + oSo);
+    int64_t* dSmp = reinterpret_cast<int64_t*>(base + oSmp);
+    double* dOut = reinterpret_cast<double*>(base + oOut);
+    hipStream_t st = h->stream;
+    TGMS_HIP(h, hipMemcpyAsync(dW, waypoints, nW * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dT, seg_times, nT * 8, hipMemcpyHostToDevice, st));
+    if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dC, coeffs, nC * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dSmp, sample_offsets, (size_t)(B + 1) * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, tgms::launch_sample(B, dSo, dW, dT, dED, dC, dt, yaw_mode, yaw_const, dSmp, dOut, st));
+    TGMS_HIP(h, hipMemcpyAsync(out, dOut, nS * TGMS_GOAL_STRIDE * 8, hipMemcpyDeviceToHost, st));
+    TGMS_HIP(h, hipStreamSynchronize(st));
+    return TGMS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,35 @@
+// tgms_internal.h — declarations shared by the kernels TU and the C-ABI TU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tgms {
+
+// Reduced-Hessian solve, uniform M (configs 2-4).  Grid: ceil(B/64) waves.
+hipError_t launch_reduced_uniform(int M, int32_t B, const double* W, const double* T,
+                                  const double* ED, double* C, int32_t* status,
+                                  hipStream_t stream);
+
+// Reduced-Hessian solve for one group of a ragged CSR batch: the n trajectories
+// perm[0..n) all have M segments (the host groups a ragged batch by M so every
+// wavefront runs a single M).
+hipError_t launch_reduced_ragged_group(int M, int32_t n, const int32_t* perm,
+                                       const int32_t* seg_offsets, const double* W,
+                                       const double* T, const double* ED, double* C,
+                                       int32_t* status, hipStream_t stream);
+
+// Dense-KKT solve (survey a1-a3 literally): one wavefront per trajectory, KKT in LDS.
+// Uniform M only (1..TGMS_DENSE_MAX_SEGMENTS); ragged batches loop over M groups.
+hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nullable*/,
+                            const int32_t* seg_offsets /*nullable if uniform*/, const double* W,
+                            const double* T, const double* ED, double* C, int32_t* status,
+                            hipStream_t stream);
+
+// Sampler: one wavefront per trajectory (grid-stride), 14 doubles per sample.
+hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,
+                         const double* ED, const double* C, double dt, int yaw_mode,
+                         double yaw_const, const int64_t* sample_offsets, double* out,
+                         hipStream_t stream);
+
+}  // namespace tgms

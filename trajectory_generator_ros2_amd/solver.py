@@ -1,0 +1,143 @@
+"""Python front-end over the C ABI (numpy host buffers or torch device tensors).
+
+Mirrors the reference's generate-then-consume flow: a batch of
+waypoint sets goes in, order-7 coefficients [seg][axis][8] come out, and the
+sampler turns them into Goal-like records at dt.  All compute runs in libtgms
+(HIP); this module only marshals pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import TgmsError
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags.c_contiguous, "arrays must be C-contiguous"
+        return a.ctypes.data
+    # torch tensor (device or host)
+    assert a.is_contiguous(), "tensors must be contiguous"
+    return a.data_ptr()
+
+
+class Solver:
+    """A libtgms handle bound to one HIP device."""
+
+    def __init__(self, device: int = 0, method: int = _lib.METHOD_REDUCED):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        st = self._L.tgms_create(ctypes.byref(h), int(device))
+        if st != _lib.OK:
+            raise TgmsError(st, "tgms_create failed (no CPU fallback exists)")
+        self._h = h
+        self.device = device
+        self.set_method(method)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.tgms_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def last_error(self) -> str:
+        return self._L.tgms_last_error(self._h).decode()
+
+    def set_method(self, method: int):
+        st = self._L.tgms_set_method(self._h, int(method))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+        self.method = method
+
+    # ---------------------------------------------------------------- host API
+    def solve(self, seg_offsets, waypoints, seg_times, end_derivs=None, check: bool = True
+              ) -> Tuple[np.ndarray, np.ndarray, int]:
+        """CSR host batch -> (coeffs [S,3,8], status [B], worst status)."""
+        so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+        W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
+        T = np.ascontiguousarray(seg_times, dtype=np.float64).reshape(-1)
+        ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
+        B = so.shape[0] - 1
+        S = int(so[-1]) if B > 0 else 0
+        C = np.zeros((S, 3, 8), dtype=np.float64)
+        st = np.zeros(max(B, 1), dtype=np.int32)
+        worst = self._L.tgms_solve_batch(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), _ptr(C), _ptr(st))
+        if check and worst not in (_lib.OK,) and worst in (_lib.ERR_DEVICE, _lib.ERR_NO_DEVICE):
+            raise TgmsError(worst, self.last_error())
+        return C, st[:B], worst
+
+    def sample(self, seg_offsets, waypoints, seg_times, end_derivs, coeffs, dt: float,
+               yaw_mode: int = _lib.YAW_CONSTANT, yaw_const: float = 0.0):
+        so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+        W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
+        T = np.ascontiguousarray(seg_times, dtype=np.float64).reshape(-1)
+        ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
+        C = np.ascontiguousarray(coeffs, dtype=np.float64)
+        B = so.shape[0] - 1
+        offs = sample_offsets(so, T, dt)
+        out = np.zeros((int(offs[-1]), _lib.GOAL_STRIDE), dtype=np.float64)
+        st = self._L.tgms_sample_batch(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), _ptr(C), float(dt),
+                                       int(yaw_mode), float(yaw_const), _ptr(offs), _ptr(out))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+        return offs, out
+
+    # -------------------------------------------------------------- device API
+    def solve_uniform_device(self, B: int, M: int, d_waypoints, d_seg_times, d_coeffs, d_status=None,
+                             d_end_derivs=None, stream: int = 0) -> None:
+        st = self._L.tgms_solve_uniform_device(self._h, int(B), int(M), _ptr(d_waypoints), _ptr(d_seg_times),
+                                               _ptr(d_end_derivs), _ptr(d_coeffs), _ptr(d_status),
+                                               ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
+    def solve_batch_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, d_coeffs,
+                           d_status=None, d_end_derivs=None, stream: int = 0) -> None:
+        so = np.ascontiguousarray(h_seg_offsets, dtype=np.int32)
+        st = self._L.tgms_solve_batch_device(self._h, int(so.shape[0] - 1), _ptr(so), _ptr(d_seg_offsets),
+                                             _ptr(d_waypoints), _ptr(d_seg_times), _ptr(d_end_derivs),
+                                             _ptr(d_coeffs), _ptr(d_status), ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
+    def sample_device(self, B: int, d_seg_offsets, d_waypoints, d_seg_times, d_coeffs, dt: float,
+                      d_sample_offsets, d_out, d_end_derivs=None, yaw_mode: int = _lib.YAW_CONSTANT,
+                      yaw_const: float = 0.0, stream: int = 0) -> None:
+        st = self._L.tgms_sample_batch_device(self._h, int(B), _ptr(d_seg_offsets), _ptr(d_waypoints),
+                                              _ptr(d_seg_times), _ptr(d_end_derivs), _ptr(d_coeffs), float(dt),
+                                              int(yaw_mode), float(yaw_const), _ptr(d_sample_offsets),
+                                              _ptr(d_out), ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
+
+def sample_count(total_T: float, dt: float) -> int:
+    return int(_lib.load().tgms_sample_count(float(total_T), float(dt)))
+
+
+def sample_offsets(seg_offsets, seg_times, dt: float) -> np.ndarray:
+    so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+    T = np.ascontiguousarray(seg_times, dtype=np.float64).reshape(-1)
+    B = so.shape[0] - 1
+    offs = np.zeros(B + 1, dtype=np.int64)
+    st = _lib.load().tgms_sample_offsets(B, _ptr(so), _ptr(T), float(dt), _ptr(offs))
+    if st != _lib.OK:
+        raise TgmsError(st, "tgms_sample_offsets")
+    return offs
