@@ -323,11 +323,15 @@ static int solve_reduced(int M, const double* W, const double* T, const double* 
                 int rx = 3 * (kx - 1) + (dx - 1);
                 for (int y = 0; y < 8; ++y) {
                     int ky = (y < 4) ? i : i + 1, dy = y & 3;
+                    if (y == 0) continue; /* folded into y == 4: KH[x][0] = -KH[x][4] */
                     if (dy != 0 && ky != 0 && ky != M) {
                         H[rx * nf + 3 * (ky - 1) + (dy - 1)] += Ks[x][y];
                     } else {
                         for (int a = 0; a < 3; ++a) {
-                            double g = (dy == 0) ? W[3 * ky + a] : end_deriv(ED, ky == 0 ? 0 : 1, dy, a);
+                            /* positions enter only through the segment displacement
+                             * (translation invariance), avoiding cancellation */
+                            double g = (dy == 0) ? W[3 * (i + 1) + a] - W[3 * i + a]
+                                                 : end_deriv(ED, ky == 0 ? 0 : 1, dy, a);
                             R[rx * 3 + a] -= Ks[x][y] * g;
                         }
                     }

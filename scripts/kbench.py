@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmark for one libtgms build (TGMS_LIB selects it):
+time the reduced solve at config 3 and check it against the oracle (reduced fp64)."""
+import json, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from trajectory_generator_ros2_amd.solver import Solver
+from trajectory_generator_ros2_amd import synthetic as S
+
+B = int(os.environ.get("KB_B", 65536)); M = int(os.environ.get("KB_M", 10)); K = 30
+so, W, T = S.uniform_batch(B, M)
+dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+dS = torch.empty((B,), dtype=torch.int32, device="cuda")
+s = Solver(0)
+sp = torch.cuda.current_stream().cuda_stream
+for _ in range(3):
+    s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+torch.cuda.synchronize()
+e0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]; e1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+for k in range(K):
+    e0[k].record(); s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp); e1[k].record()
+torch.cuda.synchronize()
+ms = sorted(e0[k].elapsed_time(e1[k]) for k in range(K))
+C = dC.cpu().numpy()
+ref_path = f"/tmp/ref_{B}_{M}.npy"
+if os.path.exists(ref_path):
+    R = np.load(ref_path)
+else:
+    from oracle import oracle as O
+    R, _ = O.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, O.KKT_C4, 16)
+    R = R.reshape(B, M, 3, 8); np.save(ref_path, R)
+err = float((np.abs(C - R).max(axis=(1, 3)) / np.abs(R).max(axis=(1, 3))).max())
+print(json.dumps({"lib": os.path.basename(os.environ.get("TGMS_LIB", "default")), "B": B, "M": M,
+                  "median_us": ms[K // 2] * 1e3, "min_us": ms[0] * 1e3,
+                  "traj_per_s": B / (ms[K // 2] * 1e-3), "max_rel_err": err,
+                  "status_ok": bool((dS == 0).all().item())}))

@@ -1,0 +1,84 @@
+"""CPU: libtgms.so builds for gfx950, loads, exports every symbol include/tgms.h
+declares, and fails loudly (no CPU fallback) when no GPU is present."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tgms.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(tgms_[a-z_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from trajectory_generator_ros2_amd import _lib
+    from trajectory_generator_ros2_amd.build import LIB_TGMS, build_tgms
+    if not os.path.exists(LIB_TGMS):
+        build_tgms()
+    return _lib.load()
+
+
+def test_header_declares_expected_api():
+    from trajectory_generator_ros2_amd._lib import EXPORTS
+    assert _declared() == sorted(EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from trajectory_generator_ros2_amd.build import LIB_TGMS
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_TGMS], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (tgms_\w+)", out))
+    for sym in _declared():
+        assert sym in exported, sym
+        assert hasattr(lib, sym)
+
+
+def test_library_contains_gfx950_code_object():
+    """The fat binary embeds an amdgcn code object for gfx950 (offload bundle id)."""
+    from trajectory_generator_ros2_amd.build import LIB_TGMS
+    blob = open(LIB_TGMS, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_no_torch_or_oracle_in_abi():
+    src = open(HEADER).read()
+    assert "torch" not in src.lower().replace("pytorch", "")
+    from trajectory_generator_ros2_amd.build import LIB_TGMS
+    out = subprocess.run(["nm", "-D", LIB_TGMS], capture_output=True, text=True, check=True).stdout
+    assert "oracle_" not in out           # the product never links the checker
+    deps = subprocess.run(["readelf", "-d", LIB_TGMS], capture_output=True, text=True, check=True).stdout
+    assert "liboracle" not in deps and "libtorch" not in deps
+
+
+def test_status_strings_and_abi_version(lib):
+    assert lib.tgms_abi_version() == 1
+    assert lib.tgms_status_string(0) == b"TGMS_OK"
+    assert lib.tgms_status_string(4) == b"TGMS_ERR_NO_DEVICE"
+    assert lib.tgms_status_string(99) == b"TGMS_ERR_UNKNOWN"
+
+
+def test_host_helpers_match_oracle_convention(lib, oracle):
+    import numpy as np
+    from trajectory_generator_ros2_amd import solver as S
+    for tot, dt in [(1.0, 0.01), (0.005, 0.01), (73.123, 0.01), (10.0, 0.1), (0.0, 0.01)]:
+        assert S.sample_count(tot, dt) == oracle.sample_count(tot, dt)
+    so = np.array([0, 3, 5], np.int32)
+    T = np.array([1.0, 2.0, 0.5, 0.25, 0.25])
+    offs = S.sample_offsets(so, T, 0.01)
+    assert list(offs) == [0, oracle.sample_count(3.5, 0.01), oracle.sample_count(3.5, 0.01) + oracle.sample_count(0.5, 0.01)]
+
+
+def test_create_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from trajectory_generator_ros2_amd import ERR_NO_DEVICE, TgmsError
+    from trajectory_generator_ros2_amd.solver import Solver
+    with pytest.raises(TgmsError) as ei:
+        Solver(0)
+    assert ei.value.status == ERR_NO_DEVICE

@@ -35,13 +35,22 @@ class TgmsError(RuntimeError):
         super().__init__(f"{status_string(status)}: {msg}" if msg else status_string(status))
 
 
-def load(path: str = LIB_TGMS):
-    """Load libtgms.so.  Raises if it is absent: build it with __graft_entry__.build()."""
+def load(path: str = ""):
+    """Load libtgms.so.  Raises if it is absent: build it with __graft_entry__.build().
+    TGMS_LIB may name an alternative build of the same ABI (kernel experiments)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("TGMS_LIB", "") or LIB_TGMS
     if not os.path.exists(path):
         raise ImportError(f"libtgms.so not built at {path}; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # PyTorch-ROCm ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Load
+    # torch first so libtgms binds to the HIP runtime instance torch uses: one runtime
+    # per process, so device pointers and streams are shared between the two.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     L.tgms_abi_version.restype = ctypes.c_int
