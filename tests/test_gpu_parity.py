@@ -221,3 +221,22 @@ def test_sampler_vs_exact_golden(solver, name):
     for f0, f1 in ((0, 3), (3, 6), (6, 9), (9, 12)):
         scale = np.abs(ref[:, f0:f1]).max()
         assert np.abs(out[:, f0:f1] - ref[:, f0:f1]).max() <= TOL * scale
+
+
+def test_sharded_solve_matches_unsharded(solver):
+    """§8(e): per-rank shards of a ragged batch solved on the GPU concatenate to the
+    unsharded GPU result bit-for-bit (trajectories are independent)."""
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(3001, 1, 16, seed=11)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+    C_all, st_all, worst = solver.solve(so, W, T)
+    assert worst == 0
+    parts, sts = [], []
+    for r in range(4):
+        sb = SH.ShardedBatch(so, W, T, None, rank=r, world=4)
+        C, st = sb.solve(lambda a, b, c, d: solver.solve(a, b, c, d)[:2])
+        parts.append(C)
+        sts.append(st[: sb.hi - sb.lo])
+    np.testing.assert_array_equal(np.concatenate(parts), C_all)
+    np.testing.assert_array_equal(np.concatenate(sts), st_all[:3001])
