@@ -1,9 +1,9 @@
 """GPU: the C++ MinSnap adapter driven like TrajectoryGenerator drives a primitive
 (readParameters -> generateTraj -> modeCB END -> generateStopTraj), checked against
 the oracle.  Reference conventions: frame_id "world" and power = true
-(Line.cpp:101-119), last goal pinned to the end point (Line.cpp:80-82), generateTraj
-appends (Line.cpp:33-97), generateStopTraj replaces and sets pub_index = 0
-(Line.cpp:120-150)."""
+(Line.cpp:91-115), last goal pinned to the end point (Line.cpp:80-82), generateTraj
+appends (Line.cpp:33-89), generateStopTraj replaces and sets pub_index = 0
+(Line.cpp:145-147)."""
 import numpy as np
 import pytest
 

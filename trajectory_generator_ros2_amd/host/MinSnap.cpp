@@ -1,8 +1,8 @@
 // MinSnap.cpp — see MinSnap.hpp.  Conventions follow the reference primitives:
-//   goal.header.frame_id = "world", goal.power = true      (Line.cpp:101-119, Circle.cpp:106/127)
+//   goal.header.frame_id = "world", goal.power = true      (Line.cpp:91-115, Circle.cpp:106/127)
 //   generation errors: log + exit(1)                         (Line.cpp:77-78, Circle.cpp:86-87)
 //   last goal pinned to the end point                        (Line.cpp:80-82; done by the sampler)
-//   "Time to calculate the traj" / "Goal vector size" logs   (Line.cpp:94-96)
+//   "Time to calculate the traj" / "Goal vector size" logs   (Line.cpp:87-88)
 #include "MinSnap.hpp"
 
 #include <algorithm>

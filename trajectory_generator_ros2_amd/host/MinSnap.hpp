@@ -8,10 +8,10 @@
 // there is no CPU path.
 //
 //   generateTraj            tgms_solve_batch (B = 1, rest-to-rest) + tgms_sample_batch at dt,
-//                           appended to goals (Line.cpp:33-97 append convention)
+//                           appended to goals (Line.cpp:33-89 append convention)
 //   generateStopTraj        one braking segment from goals[pub_index]'s p/v/a/j to rest
 //                           (end_derivs), replaces goals / index_msgs, pub_index = 0
-//                           (Line.cpp:120-150 replace convention)
+//                           (Line.cpp:145-147 replace convention)
 //   trajectoryInsideBounds  every waypoint AND every sampled position inside the room
 #pragma once
 
