@@ -51,6 +51,16 @@ def load_traffic(workload_key: str):
         return None
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(B: int, M: int, target_s: float):
     """The CPU oracle (build's own fp64 dense-KKT restatement; the reference has no
     solver) on a bounded sample of the same workload, timed on this host."""
@@ -73,9 +83,50 @@ def cpu_baseline(B: int, M: int, target_s: float):
         assert (st == 0).all()
     el = time.perf_counter() - t0
     n = n_batch * reps
+    # single-core rate on a 2048-trajectory slice (1 core and all cores)
+    t1 = time.perf_counter()
+    O.solve_batch(so[:2049], W[:2048], T[:2048], None, O.KKT_C4, 1)
+    one_core = 2048 / (time.perf_counter() - t1)
     return {"value": n / el, "unit": "trajectories/s", "cores": threads, "kind": "port",
+            "value_1core": one_core, "cpu_model": _cpu_model(),
             "sample": f"{reps} x {n_batch} trajectories of the config-3 workload (M={M}), oracle dense KKT "
                       f"(LU, partial pivoting, fp64), {threads} OpenMP thread(s), {el:.1f} s"}
+
+
+def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
+    """Sampler on the first n solved trajectories at 100 Hz:
+    Goal-layout p/v/a/j/psi/dpsi, HBM-bound by its output."""
+    import torch
+    from trajectory_generator_ros2_amd import YAW_VELOCITY
+    from trajectory_generator_ros2_amd.solver import sample_offsets
+    n = min(n, W.shape[0])
+    so = np.arange(n + 1, dtype=np.int32) * M
+    offs = sample_offsets(so, T[:n].reshape(-1), dt)
+    d_so = torch.from_numpy(so).to(dev)
+    d_offs = torch.from_numpy(offs).to(dev)
+    dWs = torch.from_numpy(np.ascontiguousarray(W[:n])).to(dev)
+    dTs = torch.from_numpy(np.ascontiguousarray(T[:n])).to(dev)
+    out = torch.empty((int(offs[-1]), 14), dtype=torch.float64, device=dev)
+    sp = stream.cuda_stream
+
+    def run():
+        solver.sample_device(n, d_so, dWs, dTs, dC, dt, d_offs, out, yaw_mode=YAW_VELOCITY, stream=sp)
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = int(offs[-1]) * 14 * 8 + n * (M * 24 * 8 + M * 8 + (M + 1) * 24 + 4 + 8)
+    return {"trajectories": n, "samples": int(offs[-1]), "dt": dt, "ms_per_launch": ms,
+            "samples_per_s": int(offs[-1]) / (ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": nbytes / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": nbytes, "kernel": "k_sample"}}
 
 
 def main():
@@ -87,7 +138,9 @@ def main():
     ap.add_argument("--segments", type=int, default=10)
     ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
     ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="0: skip the CPU baseline")
+    ap.add_argument("--sample-traj", type=int, default=4096,
+                    help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     args = ap.parse_args()
 
     import torch
@@ -131,15 +184,18 @@ def main():
     assert int((dS != 0).sum().item()) == 0, "solver reported failures"
 
     K = args.steps
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    # HIP events on the launch stream bracket the timed region; the average launch
+    # duration is their elapsed time / K (back-to-back launches, GPU never starved:
+    # host submission is a few us per launch against a ~40 us kernel).
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev0[k].record(stream)
+    ev0.record(stream)
+    for _ in range(K):
         step()
-        ev1[k].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
@@ -147,7 +203,8 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    launch_ms = float(np.mean([ev0[k].elapsed_time(ev1[k]) for k in range(K)]))
+    launch_ms = ev0.elapsed_time(ev1) / K
+    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
 
     # dense-KKT side line (the survey's literal formulation), same inputs, same GPU
     dense = None
@@ -169,6 +226,10 @@ def main():
                  "fp64_tflops_algorithmic": gfl, "fp64_peak_tflops": FP64_PEAK_TFS,
                  "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
+
+    sampler = None
+    if args.sample_traj > 0:
+        sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -206,6 +267,7 @@ def main():
                          "algorithmic_bytes_per_launch": bpl},
             "cpu_baseline": cpu,
             "dense_kkt": dense,
+            "sampler": sampler,
         }
         print(json.dumps(line), flush=True)
     solver.close()
