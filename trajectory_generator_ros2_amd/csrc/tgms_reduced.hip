@@ -32,8 +32,12 @@
 namespace tgms {
 namespace {
 
-#ifndef TGMS_MIN_WAVES
-#define TGMS_MIN_WAVES 1  // waves per SIMD the register allocation must allow
+// Waves per SIMD the register allocation must allow: two for the axis-sequential
+// solve while its state fits 256 registers without spilling (M <= 11), else one.
+#ifdef TGMS_MIN_WAVES
+#define TGMS_WAVES(M) TGMS_MIN_WAVES
+#else
+#define TGMS_WAVES(M) ((M) <= 11 ? 2 : 1)
 #endif
 
 // Scheduling fence between unrolled chain / emission steps.  The compiler-level
@@ -48,6 +52,25 @@ namespace {
 #else
 #define SCHED_FENCE() ((void)0)
 #endif
+#ifdef TGMS_STAMPS  // diagnostic build: per-wave phase timestamps (s_memtime), lane 0
+__device__ unsigned long long g_stamps[8192 * 16];
+#define STAMP(i)                                                                              \
+    do {                                                                                      \
+        asm volatile("" ::: "memory");                                                        \
+        if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define STAMP_RT(i)                                                                                  \
+    do {                                                                                             \
+        if (threadIdx.x == 0) {                                                                      \
+            g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime();            \
+            g_stamps[(size_t)blockIdx.x * 16 + 8] = __builtin_amdgcn_s_getreg((3 << 11) | 20);     \
+            g_stamps[(size_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);     \
+        }                                                                                            \
+    } while (0)
+#else
+#define STAMP(i) ((void)0)
+#define STAMP_RT(i) ((void)0)
+#endif
 #ifdef TGMS_MARKS  // phase markers in the ISA (register-pressure investigations)
 #define MARK(x) asm volatile(";MARK " #x ::: "memory")
 #else
@@ -60,17 +83,24 @@ constexpr int PSTRIDE = 33;  // LDS row stride (doubles) of the [field][trajecto
 // the 8 lanes of each ds_write_b128 group hit 8 distinct 4-bank slots.
 constexpr int OSTRIDE = 10;
 
+// One group's staged inputs, [field][trajectory] with a padded trajectory stride.
 template <int M>
-struct alignas(16) Stage {
-    // First and 16-B aligned: every ds_*_b128 on it must be naturally aligned, or
-    // the LDS replays it (SQ_LDS_UNALIGNED_STALL; cdna_hip_programming.md G17).
-    alignas(16) double O[W64 * OSTRIDE];  // one axis of one emission step, every lane
+struct In {
     double W[(M + 1) * 3 * PSTRIDE];
     double T[M * PSTRIDE];
     double R[M * PSTRIDE];  // 1/T, computed once while staging
     int64_t base[TPW];      // coefficient offset (doubles) of each slot's trajectory
     int bad[TPW];
 };
+
+template <int M>
+struct alignas(16) Stage {
+    // First and 16-B aligned: every ds_*_b128 on it must be naturally aligned, or
+    // the LDS replays it (SQ_LDS_UNALIGNED_STALL; cdna_hip_programming.md G17).
+    alignas(16) double O[W64 * OSTRIDE];  // one axis of one emission step, every lane
+    In<M> in;
+};
+
 static_assert(OSTRIDE % 2 == 0, "staged rows must keep 16-B alignment");
 
 // Per-lane view of the staged inputs in the lane's VIRTUAL frame: the even lane
@@ -88,7 +118,7 @@ struct LaneView {
 };
 
 template <int M>
-__device__ __forceinline__ LaneView make_view(const Stage<M>& sm, int slot, bool right) {
+__device__ __forceinline__ LaneView make_view(const In<M>& sm, int slot, bool right) {
     LaneView L;
     L.Wb = sm.W + (right ? M * 3 * PSTRIDE : 0) + slot;
     L.Tb = sm.T + (right ? (M - 1) * PSTRIDE : 0) + slot;
@@ -169,9 +199,15 @@ __device__ __forceinline__ void stage_axis(const OutCtx& o, const double (&c)[8]
 
 // Coefficients of one physical segment (a4 layout [axis][8]) from its end data:
 // physical start knot (w0, g0) and end knot (w1, g1), g = (v, a, j) x axis.
+struct NoHook {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+// `hook(a)` runs after axis a is handed to the store path (software pipelining).
+template <class Hook = NoHook>
 __device__ __forceinline__ void emit_step(const OutCtx& o, double T, double r, const double* w0, const double* w1,
                                           const double (&g0)[3][3], const double (&g1)[3][3], int segL, int segR,
-                                          bool has_r) {
+                                          bool has_r, Hook&& hook = Hook()) {
     const double T2 = T * T, T3 = T2 * T;
     double rp[8];
     rpowers(r, rp);
@@ -191,15 +227,17 @@ __device__ __forceinline__ void emit_step(const OutCtx& o, double T, double r, c
                           (1.0 / 6.0) * h7;
         const double c[8] = {w0[a], v0, 0.5 * a0, j0 * (1.0 / 6.0), d4 * rp[4], d5 * rp[5], d6 * rp[6], d7 * rp[7]};
         stage_axis(o, c, a, segL, segR, has_r);
+        hook(a);
     }
 }
 
 // Emit virtual segment e (virtual knots e .. e+1, derivatives xs / xe).  The even
 // lane's virtual segment e is physical segment e; the odd lane's is physical
 // segment M-1-e traversed backwards (physical start = virtual knot e+1, with P).
-template <int M>
+template <int M, class Hook = NoHook>
 __device__ __forceinline__ void emit_virtual(const OutCtx& o, const LaneView& L, bool right, int e,
-                                             const double (&xs)[3][3], const double (&xe)[3][3], bool has_r) {
+                                             const double (&xs)[3][3], const double (&xe)[3][3], bool has_r,
+                                             Hook&& hook = Hook()) {
     const double sg = right ? -1.0 : 1.0;
     double g0[3][3], g1[3][3], w0[3], w1[3];
 #pragma unroll
@@ -214,7 +252,7 @@ __device__ __forceinline__ void emit_virtual(const OutCtx& o, const LaneView& L,
             g1[d][a] = right ? f * xs[d][a] : xe[d][a];
         }
     }
-    emit_step(o, L.t(e), L.r(e), w0, w1, g0, g1, e, M - 1 - e, has_r);
+    emit_step(o, L.t(e), L.r(e), w0, w1, g0, g1, e, M - 1 - e, has_r, hook);
 }
 
 // ---------------------------------------------------------------------------
@@ -298,14 +336,33 @@ __device__ __forceinline__ void coupling(const double (&p)[8], double (&B)[3][3]
 }
 
 // ---------------------------------------------------------------------------
-// One trajectory on a lane pair.  Invalid trajectories were replaced by an
-// all-zero, unit-time one during staging, so they come out as exact zeros.
-// Returns the status (meaningful on both lanes).
+// One trajectory on a lane pair, as explicit phases over a PairState so that two
+// groups can be software-pipelined in one wavefront (k_reduced_pipe): the chain of
+// the next group runs between the emission steps of the current one.
+// Invalid trajectories were replaced by an all-zero, unit-time one during staging,
+// so they come out as exact zeros.
+template <int M>
+struct Chain {
+    static constexpr int c = (M - 1) / 2;  // even chain: knots 1..c, odd chain: M-1..c+1
+    static constexpr int nL = c, nR = M - 1 - c, NS = nR;
+    static constexpr int NE = nL + 1;      // emission steps (even lane: nL+1 segments, odd: nR)
+};
+
+template <int M>
+struct PairState {
+    Ldl3 F[Chain<M>::NS];
+    double Y[Chain<M>::NS + 1][3][3];  // chain right-hand sides, then knot derivatives
+    double u0[3][3], uM[3][3];         // virtual-frame end derivatives [derivative][axis]
+    double pp[8];                      // powers of r of the segment left of the next knot
+    Sym3 Dl;                           // last pivot block of this lane's chain
+    double fin;                        // sum of the solved knot derivatives (finiteness)
+    bool spd;
+};
+
 template <int M, bool HAS_ED>
-__device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, bool valid,
-                                              const double* __restrict__ ed, const OutCtx& O) {
-    // virtual-frame end derivatives: even lane (u0, uM); odd lane (P uM, P u0)
-    double u0[3][3], uM[3][3];  // [derivative][axis]
+__device__ __forceinline__ void ps_init(PairState<M>& S, const LaneView& L, bool right, bool valid,
+                                        const double* __restrict__ ed) {
+    // even lane (u0, uM); odd lane (P uM, P u0)
     const double sg = right ? -1.0 : 1.0;
 #pragma unroll
     for (int d = 0; d < 3; ++d)
@@ -314,176 +371,467 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
             const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
             const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
             const double f = (d == 1) ? 1.0 : sg;
-            u0[d][a] = right ? f * s1 : s0;
-            uM[d][a] = right ? f * s0 : s1;
+            S.u0[d][a] = right ? f * s1 : s0;
+            S.uM[d][a] = right ? f * s0 : s1;
         }
-    bool spd = true;
-    double fin = 0.0;  // sum of the solved knot derivatives (non-finite check)
+    S.spd = true;
+    S.fin = 0.0;
+    if constexpr (M >= 3) rpowers(L.r(0), S.pp);
+}
 
-#ifdef TGMS_ABL_NOCOMPUTE  // ablation: staging + emission only, knot derivatives = 0
-    if constexpr (true) {
+// Elimination step s (virtual knot k = s+1) of the lane's chain, in three parts
+// so that it can be spread between the three axes of an emission step:
+//   0: diagonal block and right-hand side of knot k
+//   1: right-hand side update with the previous knot's solve
+//   2: Schur update of the diagonal block and its LDL^T
+struct ChainTmp {
+    Sym3 D;
+    double y[3][3];
+    double pn[8];
+};
+
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void ps_chain_part(PairState<M>& S, ChainTmp& X, const LaneView& L, bool right, int s,
+                                              int part) {
+    using CH = Chain<M>;
+    const int k = s + 1;
+    if (part == 0) {
+        rpowers(L.r(k), X.pn);
+        X.D = knot_diag(S.pp, X.pn);
+        knot_rhs<HAS_ED>(L, k, S.pp, X.pn, S.u0, X.y);
+    } else if (part == 1) {
+        if (s >= 1) {
+            double B[3][3];
+            coupling(S.pp, B);  // H_{k-1, k}
 #pragma unroll
-        for (int e = 0; e < (M + 1) / 2; ++e) emit_virtual<M>(O, L, right, e, u0, uM, e < M / 2);
-    } else
-#endif
-    if constexpr (M == 1) {
-        emit_virtual<M>(O, L, right, 0, u0, uM, false);
-    } else if constexpr (M == 2) {
-        // one interior knot: virtual knot 1 on both lanes (physical 1 for both)
-        double pp[8], pn[8], y[3][3], x[3][3];
-        rpowers(L.r(0), pp);
-        rpowers(L.r(1), pn);
-        const Sym3 D = knot_diag(pp, pn);
-        knot_rhs<HAS_ED>(L, 1, pp, pn, u0, y);
-        if (HAS_ED) {  // final derivatives through C_1 (virtual segment 1)
-            double C1[3][3];
-            coupling(pn, C1);
+            for (int a = 0; a < 3; ++a) {
+                double v0, v1, v2;
+                ldl3_solve(S.F[s - 1], S.Y[s - 1][0][a], S.Y[s - 1][1][a], S.Y[s - 1][2][a], v0, v1, v2);
 #pragma unroll
-            for (int d = 0; d < 3; ++d)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) y[d][a] -= C1[d][0] * uM[0][a] + C1[d][1] * uM[1][a] + C1[d][2] * uM[2][a];
+                for (int d = 0; d < 3; ++d) X.y[d][a] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
+            }
         }
-        const Ldl3 f = ldl3s(D, spd);
+    } else {
+        const int nl = right ? CH::nR : CH::nL;
+        Sym3 D = X.D;
+        if (s >= 1) {
+            double B[3][3], Wc[3][3];
+            coupling(S.pp, B);
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+                ldl3_solve(S.F[s - 1], B[0][e], B[1][e], B[2][e], Wc[0][e], Wc[1][e], Wc[2][e]);
+            sym_sub_btw(D, B, Wc);
+        }
+        bool ok;
+        S.F[s] = ldl3s(D, ok);
+        S.spd = S.spd && (ok || s >= nl);
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) S.Y[s][d][a] = X.y[d][a];
+        if (s == CH::nL - 1) S.Dl = D;
+        if (CH::nR > CH::nL && s == CH::nR - 1) {
+            S.Dl.a00 = right ? D.a00 : S.Dl.a00;
+            S.Dl.a01 = right ? D.a01 : S.Dl.a01;
+            S.Dl.a02 = right ? D.a02 : S.Dl.a02;
+            S.Dl.a11 = right ? D.a11 : S.Dl.a11;
+            S.Dl.a12 = right ? D.a12 : S.Dl.a12;
+            S.Dl.a22 = right ? D.a22 : S.Dl.a22;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) S.pp[q] = X.pn[q];
+    }
+}
+
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void ps_chain_step(PairState<M>& S, const LaneView& L, bool right, int s) {
+    ChainTmp X;
+    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 0);
+    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 1);
+    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 2);
+}
+
+// Interface (physical knots c and c+1) and back substitution: afterwards Y[0..NS]
+// hold the knot derivatives of virtual knots 1..NS+1 (Y[nl] = the other lane's
+// interface knot).
+template <int M>
+__device__ __forceinline__ void ps_finish(PairState<M>& S, const LaneView& L, bool right) {
+    using CH = Chain<M>;
+    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS;
+    const int nl = right ? nR : nL;
+    const double sg = right ? -1.0 : 1.0;
+    MARK(interface);
+    STAMP(2);
+    SCHED_FENCE();
+    // Each lane maps its last pivot block / right-hand side to the physical frame
+    // (P flips exactly), the even and odd lane broadcast theirs, and both lanes
+    // solve the same 6x6 system with bit-identical operations: x_c by the Schur
+    // complement onto knot c, then x_{c+1} back-solved from it.  (Two independent
+    // Schur solves leave x_c / x_{c+1} mutually inconsistent: ~70x less accurate.)
+    double xm[3][3];
+    {
+        Sym3 DL, DR;
+        {
+            const double p01 = sg * S.Dl.a01, p12 = sg * S.Dl.a12;
+            DL = Sym3{pair_even(S.Dl.a00), pair_even(p01), pair_even(S.Dl.a02),
+                      pair_even(S.Dl.a11), pair_even(p12), pair_even(S.Dl.a22)};
+            DR = Sym3{pair_odd(S.Dl.a00), pair_odd(p01), pair_odd(S.Dl.a02),
+                      pair_odd(S.Dl.a11), pair_odd(p12), pair_odd(S.Dl.a22)};
+        }
+        double Cc[3][3];  // H_{c, c+1}: physical segment c = virtual segment nl on both lanes
+        {
+            double pc[8];
+            rpowers(L.r(nl), pc);
+            coupling(pc, Cc);
+        }
+        bool ok1, ok2;
+        const Ldl3 FR = ldl3s(DR, ok1);
+        {
+            double Wm[3][3];
+#pragma unroll
+            for (int e = 0; e < 3; ++e) ldl3_solve(FR, Cc[e][0], Cc[e][1], Cc[e][2], Wm[0][e], Wm[1][e], Wm[2][e]);
+            DL.a00 -= Cc[0][0] * Wm[0][0] + Cc[0][1] * Wm[1][0] + Cc[0][2] * Wm[2][0];
+            DL.a01 -= Cc[0][0] * Wm[0][1] + Cc[0][1] * Wm[1][1] + Cc[0][2] * Wm[2][1];
+            DL.a02 -= Cc[0][0] * Wm[0][2] + Cc[0][1] * Wm[1][2] + Cc[0][2] * Wm[2][2];
+            DL.a11 -= Cc[1][0] * Wm[0][1] + Cc[1][1] * Wm[1][1] + Cc[1][2] * Wm[2][1];
+            DL.a12 -= Cc[1][0] * Wm[0][2] + Cc[1][1] * Wm[1][2] + Cc[1][2] * Wm[2][2];
+            DL.a22 -= Cc[2][0] * Wm[0][2] + Cc[2][1] * Wm[1][2] + Cc[2][2] * Wm[2][2];
+        }
+        const Ldl3 FS = ldl3s(DL, ok2);
+        S.spd = S.spd && ok1 && ok2;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            ldl3_solve(f, y[0][a], y[1][a], y[2][a], x[0][a], x[1][a], x[2][a]);
-            fin += (x[0][a] + x[1][a]) + x[2][a];
-        }
-        emit_virtual<M>(O, L, right, 0, u0, x, true);
-    } else {
-        constexpr int c = (M - 1) / 2;  // even chain: knots 1..c, odd chain: M-1..c+1
-        constexpr int nL = c, nR = M - 1 - c, NS = nR;
-        const int nl = right ? nR : nL;
-        Ldl3 F[NS];
-        double Y[NS + 1][3][3];  // chain right-hand sides, then knot derivatives; Y[nl] = other interface knot
-        Sym3 Dl;
-        MARK(chain);
-        // ---- elimination along the lane's virtual chain, knots 1..nl ----
-        double pp[8], pn[8];  // powers of r of the segments left / right of the current knot
-        rpowers(L.r(0), pp);
+            double yL[3], yR[3];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            SCHED_FENCE();
-            const int k = s + 1;
-            rpowers(L.r(k), pn);
-            Sym3 D = knot_diag(pp, pn);
-            double y[3][3];
-            knot_rhs<HAS_ED>(L, k, pp, pn, u0, y);
-            if (s >= 1) {
-                double B[3][3], Wc[3][3];
-                coupling(pp, B);  // H_{k-1, k}
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    double v0, v1, v2;
-                    ldl3_solve(F[s - 1], Y[s - 1][0][a], Y[s - 1][1][a], Y[s - 1][2][a], v0, v1, v2);
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) y[d][a] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
-                }
-#pragma unroll
-                for (int e = 0; e < 3; ++e) ldl3_solve(F[s - 1], B[0][e], B[1][e], B[2][e], Wc[0][e], Wc[1][e], Wc[2][e]);
-                sym_sub_btw(D, B, Wc);
+            for (int d = 0; d < 3; ++d) {
+                // this lane's last chain right-hand side Y[nl-1], in the physical frame
+                const double yv = (nR > nL) ? (right ? S.Y[NS - 1][d][a] : S.Y[nL - 1][d][a]) : S.Y[nL - 1][d][a];
+                const double yp = (d == 1) ? yv : sg * yv;
+                yL[d] = pair_even(yp);
+                yR[d] = pair_odd(yp);
             }
-            bool ok;
-            F[s] = ldl3s(D, ok);
-            spd = spd && (ok || s >= nl);
+            double g0, g1, g2;
+            ldl3_solve(FR, yR[0], yR[1], yR[2], g0, g1, g2);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
+            double xc0, xc1, xc2, x10, x11, x12;
+            ldl3_solve(FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
+            const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
+            const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
+            const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
+            ldl3_solve(FR, b0, b1, b2, x10, x11, x12);
+            // own / other interface knot in the lane's virtual frame
+            xm[0][a] = right ? -x10 : xc0;
+            xm[1][a] = right ? x11 : xc1;
+            xm[2][a] = right ? -x12 : xc2;
+            const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
+            if (nR > nL) {  // the other knot goes to slot nl: nL (even) / nR (odd)
+                S.Y[nL][0][a] = right ? S.Y[nL][0][a] : o0;
+                S.Y[nL][1][a] = right ? S.Y[nL][1][a] : o1;
+                S.Y[nL][2][a] = right ? S.Y[nL][2][a] : o2;
+                S.Y[nR][0][a] = right ? o0 : S.Y[nR][0][a];
+                S.Y[nR][1][a] = right ? o1 : S.Y[nR][1][a];
+                S.Y[nR][2][a] = right ? o2 : S.Y[nR][2][a];
+            } else {
+                S.Y[nL][0][a] = o0;
+                S.Y[nL][1][a] = o1;
+                S.Y[nL][2][a] = o2;
+            }
+            S.fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
+        }
+    }
+    MARK(backsub);
+    STAMP(3);
+    // ---- back substitution along the virtual chain: x_s = F_s^{-1}(y_s - C_{s+1} x_{s+1}) ----
+#pragma unroll
+    for (int s = NS - 1; s >= 0; --s) {
+        SCHED_FENCE();
+        const bool at_end = (s == nl - 1);
+        const bool inside = (s < nl - 1);
+        if (s + 1 < NS) {
+            double B[3][3];
+            {
+                double pb[8];
+                rpowers(L.r(s + 1), pb);
+                coupling(pb, B);  // H_{s+1, s+2} (virtual knots)
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double b[3], x0, x1, x2;
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+                    b[d] = S.Y[s][d][a] - (B[d][0] * S.Y[s + 1][0][a] + B[d][1] * S.Y[s + 1][1][a] + B[d][2] * S.Y[s + 1][2][a]);
+                ldl3_solve(S.F[s], b[0], b[1], b[2], x0, x1, x2);
+                S.Y[s][0][a] = at_end ? xm[0][a] : (inside ? x0 : S.Y[s][0][a]);
+                S.Y[s][1][a] = at_end ? xm[1][a] : (inside ? x1 : S.Y[s][1][a]);
+                S.Y[s][2][a] = at_end ? xm[2][a] : (inside ? x2 : S.Y[s][2][a]);
+                S.fin += inside ? (x0 + x1) + x2 : 0.0;
+            }
+        } else {
 #pragma unroll
             for (int d = 0; d < 3; ++d)
 #pragma unroll
-                for (int a = 0; a < 3; ++a) Y[s][d][a] = y[d][a];
-            if (s == nL - 1) Dl = D;
-            if (nR > nL && s == nR - 1) {
-                Dl.a00 = right ? D.a00 : Dl.a00;
-                Dl.a01 = right ? D.a01 : Dl.a01;
-                Dl.a02 = right ? D.a02 : Dl.a02;
-                Dl.a11 = right ? D.a11 : Dl.a11;
-                Dl.a12 = right ? D.a12 : Dl.a12;
-                Dl.a22 = right ? D.a22 : Dl.a22;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+                for (int a = 0; a < 3; ++a) S.Y[s][d][a] = at_end ? xm[d][a] : S.Y[s][d][a];
         }
-        MARK(interface);
+    }
+    MARK(emission);
+    STAMP(4);
+}
+
+// Emission step e: virtual segment e = virtual knots e..e+1.
+template <int M, class Hook = NoHook>
+__device__ __forceinline__ void ps_emit_step(const PairState<M>& S, const OutCtx& O, const LaneView& L, bool right,
+                                             int e, Hook&& hook = Hook()) {
+    using CH = Chain<M>;
+    double xs[3][3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) xs[d][a] = (e == 0) ? S.u0[d][a] : S.Y[e >= 1 ? e - 1 : 0][d][a];
+    emit_virtual<M>(O, L, right, e, xs, S.Y[e], e < CH::nR, hook);
+}
+
+template <int M>
+__device__ __forceinline__ int32_t ps_status(const PairState<M>& S, bool valid) {
+    const bool spd_pair = S.spd && (pair_swap(S.spd ? 1.0 : 0.0) != 0.0);
+    const double fin_pair = S.fin + pair_swap(S.fin);
+    if (!valid) return TGMS_ERR_INVALID_ARG;
+    if (!spd_pair) return TGMS_ERR_SINGULAR;
+    if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
+    return TGMS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Axis-sequential solve (default for M >= 3).  The 3x3 block factorisation is
+// shared by the three axes, but the right-hand sides are not: factor once, then
+// run forward substitution, interface, back substitution and emission one axis at
+// a time.  Only the factors and ONE axis' knot derivatives are live at once
+// (~100 doubles per lane instead of ~160), which lets two waves share a SIMD:
+// one wave's FP64 dependency chains, LDS round trips and store stalls are hidden
+// behind the other's work.  Same arithmetic, in the same order per axis, as the
+// joint solve above.
+template <int M>
+struct AxFactors {
+    Ldl3 F[Chain<M>::NS];
+    Ldl3 FR, FS;       // interface: odd-side pivot block, Schur complement onto knot c
+    double Cc[3][3];   // H_{c, c+1}
+    bool spd;
+};
+
+template <int M>
+__device__ __forceinline__ void ax_factor(AxFactors<M>& Fa, const LaneView& L, bool right) {
+    using CH = Chain<M>;
+    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS;
+    const int nl = right ? nR : nL;
+    const double sg = right ? -1.0 : 1.0;
+    Fa.spd = true;
+    Sym3 Dl;
+    double pp[8];
+    rpowers(L.r(0), pp);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
         SCHED_FENCE();
-        // ---- interface: physical knots c (even chain's last) and c+1 (odd's) ----
-        // Each lane maps its last pivot block / right-hand side to the physical frame
-        // (P flips exactly), the even and odd lane broadcast theirs, and both lanes
-        // solve the same 6x6 system with bit-identical operations: x_c by the Schur
-        // complement onto knot c, then x_{c+1} back-solved from it.  (Two independent
-        // Schur solves leave x_c / x_{c+1} mutually inconsistent: ~70x less accurate.)
-        double xm[3][3];
+        const int k = s + 1;
+        double pn[8];
+        rpowers(L.r(k), pn);
+        Sym3 D = knot_diag(pp, pn);
+        if (s >= 1) {
+            double B[3][3], Wc[3][3];
+            coupling(pp, B);  // H_{k-1, k}
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+                ldl3_solve(Fa.F[s - 1], B[0][e], B[1][e], B[2][e], Wc[0][e], Wc[1][e], Wc[2][e]);
+            sym_sub_btw(D, B, Wc);
+        }
+        bool ok;
+        Fa.F[s] = ldl3s(D, ok);
+        Fa.spd = Fa.spd && (ok || s >= nl);
+        if (s == nL - 1) Dl = D;
+        if (nR > nL && s == nR - 1) {
+            Dl.a00 = right ? D.a00 : Dl.a00;
+            Dl.a01 = right ? D.a01 : Dl.a01;
+            Dl.a02 = right ? D.a02 : Dl.a02;
+            Dl.a11 = right ? D.a11 : Dl.a11;
+            Dl.a12 = right ? D.a12 : Dl.a12;
+            Dl.a22 = right ? D.a22 : Dl.a22;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+    }
+    SCHED_FENCE();
+    // interface blocks in the physical frame, broadcast from both lanes of the pair
+    Sym3 DL, DR;
+    {
+        const double p01 = sg * Dl.a01, p12 = sg * Dl.a12;
+        DL = Sym3{pair_even(Dl.a00), pair_even(p01), pair_even(Dl.a02),
+                  pair_even(Dl.a11), pair_even(p12), pair_even(Dl.a22)};
+        DR = Sym3{pair_odd(Dl.a00), pair_odd(p01), pair_odd(Dl.a02),
+                  pair_odd(Dl.a11), pair_odd(p12), pair_odd(Dl.a22)};
+    }
+    {
+        double pc[8];
+        rpowers(L.r(nl), pc);  // physical segment c = virtual segment nl on both lanes
+        coupling(pc, Fa.Cc);
+    }
+    bool ok1, ok2;
+    Fa.FR = ldl3s(DR, ok1);
+    {
+        double Wm[3][3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+            ldl3_solve(Fa.FR, Fa.Cc[e][0], Fa.Cc[e][1], Fa.Cc[e][2], Wm[0][e], Wm[1][e], Wm[2][e]);
+        const double(&Cc)[3][3] = Fa.Cc;
+        DL.a00 -= Cc[0][0] * Wm[0][0] + Cc[0][1] * Wm[1][0] + Cc[0][2] * Wm[2][0];
+        DL.a01 -= Cc[0][0] * Wm[0][1] + Cc[0][1] * Wm[1][1] + Cc[0][2] * Wm[2][1];
+        DL.a02 -= Cc[0][0] * Wm[0][2] + Cc[0][1] * Wm[1][2] + Cc[0][2] * Wm[2][2];
+        DL.a11 -= Cc[1][0] * Wm[0][1] + Cc[1][1] * Wm[1][1] + Cc[1][2] * Wm[2][1];
+        DL.a12 -= Cc[1][0] * Wm[0][2] + Cc[1][1] * Wm[1][2] + Cc[1][2] * Wm[2][2];
+        DL.a22 -= Cc[2][0] * Wm[0][2] + Cc[2][1] * Wm[1][2] + Cc[2][2] * Wm[2][2];
+    }
+    Fa.FS = ldl3s(DL, ok2);
+    Fa.spd = Fa.spd && ok1 && ok2;
+}
+
+// Right-hand side of virtual knot k for axis a (see knot_rhs).
+template <bool HAS_ED>
+__device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, const double (&pp)[8],
+                                              const double (&pn)[8], const double (&u0)[3], double (&y)[3]) {
+    const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
+    const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+    const double wk = L.w(k, a);
+    const double dp = wk - L.w(k - 1, a);
+    const double dn = L.w(k + 1, a) - wk;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) y[d] = fp[d] * dp + fn[d] * dn;
+    if (HAS_ED && k == 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) y[d] -= (KSE[e][d] * pp[5 - d - e]) * u0[e];
+    }
+}
+
+// Coefficients of axis a of virtual segment e (knots e, e+1 with derivatives xs, xe).
+template <int M>
+__device__ __forceinline__ void emit_axis(const OutCtx& o, const LaneView& L, bool right, int e, int a,
+                                          const double (&xs)[3], const double (&xe)[3], bool has_r) {
+    const double ws = L.w(e, a), we = L.w(e + 1, a);
+    const double w0 = right ? we : ws, w1 = right ? ws : we;
+    // the odd lane runs the segment backwards: physical start = virtual knot e+1, with P
+    const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
+    const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
+    const double T = L.t(e), r = L.r(e);
+    const double T2 = T * T, T3 = T2 * T;
+    const double r2 = r * r, r4 = r2 * r2, r5 = r4 * r, r6 = r4 * r2, r7 = r6 * r;
+    const double dw = w1 - w0;
+    const double h1 = T * v0, h2 = T2 * a0, h3 = T3 * j0;
+    const double h5 = T * v1, h6 = T2 * a1, h7 = T3 * j1;
+    const double d4 = 35.0 * dw - 20.0 * h1 - 5.0 * h2 - (2.0 / 3.0) * h3 - 15.0 * h5 + 2.5 * h6 - (1.0 / 6.0) * h7;
+    const double d5 = -84.0 * dw + 45.0 * h1 + 10.0 * h2 + h3 + 39.0 * h5 - 7.0 * h6 + 0.5 * h7;
+    const double d6 = 70.0 * dw - 36.0 * h1 - 7.5 * h2 - (2.0 / 3.0) * h3 - 34.0 * h5 + 6.5 * h6 - 0.5 * h7;
+    const double d7 = -20.0 * dw + 10.0 * h1 + 2.0 * h2 + (1.0 / 6.0) * h3 + 10.0 * h5 - 2.0 * h6 + (1.0 / 6.0) * h7;
+    const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), d4 * r4, d5 * r5, d6 * r6, d7 * r7};
+    stage_axis(o, c, a, e, M - 1 - e, has_r);
+}
+
+template <int M, bool HAS_ED>
+__device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, bool valid,
+                                                 const double* __restrict__ ed, const OutCtx& O) {
+    using CH = Chain<M>;
+    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS, NE = CH::NE;
+    const int nl = right ? nR : nL;
+    const double sg = right ? -1.0 : 1.0;
+    MARK(chain);
+    AxFactors<M> Fa;
+    ax_factor<M>(Fa, L, right);
+    double fin = 0.0;
+#pragma unroll 1
+    for (int a = 0; a < 3; ++a) {
+        // virtual-frame start derivatives of this axis: even lane u0, odd lane P uM
+        double u0[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
+            const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
+            u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
+        }
+        // ---- forward substitution ----
+        double Y[NS + 1][3];
         {
-            Sym3 DL, DR;
-            {
-                const double p01 = sg * Dl.a01, p12 = sg * Dl.a12;
-                DL = Sym3{pair_even(Dl.a00), pair_even(p01), pair_even(Dl.a02),
-                          pair_even(Dl.a11), pair_even(p12), pair_even(Dl.a22)};
-                DR = Sym3{pair_odd(Dl.a00), pair_odd(p01), pair_odd(Dl.a02),
-                          pair_odd(Dl.a11), pair_odd(p12), pair_odd(Dl.a22)};
+            double pp[8];
+            rpowers(L.r(0), pp);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                SCHED_FENCE();
+                const int k = s + 1;
+                double pn[8];
+                rpowers(L.r(k), pn);
+                double y[3];
+                knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
+                if (s >= 1) {
+                    double B[3][3], v0, v1, v2;
+                    coupling(pp, B);
+                    ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
+                }
+#pragma unroll
+                for (int d = 0; d < 3; ++d) Y[s][d] = y[d];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pp[q] = pn[q];
             }
-            double Cc[3][3];  // H_{c, c+1}: physical segment c = virtual segment nl on both lanes
+        }
+        SCHED_FENCE();
+        // ---- interface (bit-identical on both lanes, see ps_finish) ----
+        double xm[3];
+        {
+            double yL[3], yR[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const double yv = (nR > nL) ? (right ? Y[NS - 1][d] : Y[nL - 1][d]) : Y[nL - 1][d];
+                const double yp = (d == 1) ? yv : sg * yv;
+                yL[d] = pair_even(yp);
+                yR[d] = pair_odd(yp);
+            }
+#ifdef TGMS_AX_KEEP_CC
+            const double(&Cc)[3][3] = Fa.Cc;
+#else  // recomputed per axis: 18 fewer live registers across the axis loop
+            double Cc[3][3];
             {
                 double pc[8];
                 rpowers(L.r(nl), pc);
                 coupling(pc, Cc);
             }
-            bool ok1, ok2;
-            const Ldl3 FR = ldl3s(DR, ok1);
-            {
-                double Wm[3][3];
+#endif
+            double g0, g1, g2;
+            ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
 #pragma unroll
-                for (int e = 0; e < 3; ++e) ldl3_solve(FR, Cc[e][0], Cc[e][1], Cc[e][2], Wm[0][e], Wm[1][e], Wm[2][e]);
-                DL.a00 -= Cc[0][0] * Wm[0][0] + Cc[0][1] * Wm[1][0] + Cc[0][2] * Wm[2][0];
-                DL.a01 -= Cc[0][0] * Wm[0][1] + Cc[0][1] * Wm[1][1] + Cc[0][2] * Wm[2][1];
-                DL.a02 -= Cc[0][0] * Wm[0][2] + Cc[0][1] * Wm[1][2] + Cc[0][2] * Wm[2][2];
-                DL.a11 -= Cc[1][0] * Wm[0][1] + Cc[1][1] * Wm[1][1] + Cc[1][2] * Wm[2][1];
-                DL.a12 -= Cc[1][0] * Wm[0][2] + Cc[1][1] * Wm[1][2] + Cc[1][2] * Wm[2][2];
-                DL.a22 -= Cc[2][0] * Wm[0][2] + Cc[2][1] * Wm[1][2] + Cc[2][2] * Wm[2][2];
+            for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
+            double xc0, xc1, xc2, x10, x11, x12;
+            ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
+            const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
+            const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
+            const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
+            ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
+            xm[0] = right ? -x10 : xc0;
+            xm[1] = right ? x11 : xc1;
+            xm[2] = right ? -x12 : xc2;
+            const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
+            if (nR > nL) {
+                Y[nL][0] = right ? Y[nL][0] : o0;
+                Y[nL][1] = right ? Y[nL][1] : o1;
+                Y[nL][2] = right ? Y[nL][2] : o2;
+                Y[nR][0] = right ? o0 : Y[nR][0];
+                Y[nR][1] = right ? o1 : Y[nR][1];
+                Y[nR][2] = right ? o2 : Y[nR][2];
+            } else {
+                Y[nL][0] = o0;
+                Y[nL][1] = o1;
+                Y[nL][2] = o2;
             }
-            const Ldl3 FS = ldl3s(DL, ok2);
-            spd = spd && ok1 && ok2;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double yL[3], yR[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    // this lane's last chain right-hand side Y[nl-1], in the physical frame
-                    const double yv = (nR > nL) ? (right ? Y[NS - 1][d][a] : Y[nL - 1][d][a]) : Y[nL - 1][d][a];
-                    const double yp = (d == 1) ? yv : sg * yv;
-                    yL[d] = pair_even(yp);
-                    yR[d] = pair_odd(yp);
-                }
-                double g0, g1, g2;
-                ldl3_solve(FR, yR[0], yR[1], yR[2], g0, g1, g2);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
-                double xc0, xc1, xc2, x10, x11, x12;
-                ldl3_solve(FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
-                const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
-                const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
-                const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
-                ldl3_solve(FR, b0, b1, b2, x10, x11, x12);
-                // own / other interface knot in the lane's virtual frame
-                xm[0][a] = right ? -x10 : xc0;
-                xm[1][a] = right ? x11 : xc1;
-                xm[2][a] = right ? -x12 : xc2;
-                const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
-                if (nR > nL) {  // the other knot goes to slot nl: nL (even) / nR (odd)
-                    Y[nL][0][a] = right ? Y[nL][0][a] : o0;
-                    Y[nL][1][a] = right ? Y[nL][1][a] : o1;
-                    Y[nL][2][a] = right ? Y[nL][2][a] : o2;
-                    Y[nR][0][a] = right ? o0 : Y[nR][0][a];
-                    Y[nR][1][a] = right ? o1 : Y[nR][1][a];
-                    Y[nR][2][a] = right ? o2 : Y[nR][2][a];
-                } else {
-                    Y[nL][0][a] = o0;
-                    Y[nL][1][a] = o1;
-                    Y[nL][2][a] = o2;
-                }
-                fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
-            }
+            fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
         }
-        MARK(backsub);
-        // ---- back substitution along the virtual chain: x_s = F_s^{-1}(y_s - C_{s+1} x_{s+1}) ----
+        // ---- back substitution ----
 #pragma unroll
         for (int s = NS - 1; s >= 0; --s) {
             SCHED_FENCE();
@@ -494,52 +842,32 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
                 {
                     double pb[8];
                     rpowers(L.r(s + 1), pb);
-                    coupling(pb, B);  // H_{s+1, s+2} (virtual knots)
+                    coupling(pb, B);
                 }
+                double b[3], x0, x1, x2;
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    double b[3], x0, x1, x2;
-#pragma unroll
-                    for (int d = 0; d < 3; ++d)
-                        b[d] = Y[s][d][a] - (B[d][0] * Y[s + 1][0][a] + B[d][1] * Y[s + 1][1][a] + B[d][2] * Y[s + 1][2][a]);
-                    ldl3_solve(F[s], b[0], b[1], b[2], x0, x1, x2);
-                    Y[s][0][a] = at_end ? xm[0][a] : (inside ? x0 : Y[s][0][a]);
-                    Y[s][1][a] = at_end ? xm[1][a] : (inside ? x1 : Y[s][1][a]);
-                    Y[s][2][a] = at_end ? xm[2][a] : (inside ? x2 : Y[s][2][a]);
-                    fin += inside ? (x0 + x1) + x2 : 0.0;
-                }
+                for (int d = 0; d < 3; ++d) b[d] = Y[s][d] - (B[d][0] * Y[s + 1][0] + B[d][1] * Y[s + 1][1] + B[d][2] * Y[s + 1][2]);
+                ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
+                Y[s][0] = at_end ? xm[0] : (inside ? x0 : Y[s][0]);
+                Y[s][1] = at_end ? xm[1] : (inside ? x1 : Y[s][1]);
+                Y[s][2] = at_end ? xm[2] : (inside ? x2 : Y[s][2]);
+                fin += inside ? (x0 + x1) + x2 : 0.0;
             } else {
 #pragma unroll
-                for (int d = 0; d < 3; ++d)
-#pragma unroll
-                    for (int a = 0; a < 3; ++a) Y[s][d][a] = at_end ? xm[d][a] : Y[s][d][a];
+                for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
             }
         }
-        MARK(emission);
-#ifdef TGMS_ABL_NOEMIT  // ablation (register study): consume the knot derivatives, emit nothing
-#pragma unroll
-        for (int e = 0; e <= NS; ++e)
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) asm volatile("" ::"v"(Y[e][d][a]));
-#else
-        // ---- coefficients: virtual segment e = virtual knots e..e+1 ----
-        constexpr int NE = nL + 1;  // even lane: nL+1 segments; odd lane: nR (<= nL+1)
+        // ---- emission of this axis ----
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             SCHED_FENCE();
-            double xs[3][3];
+            double xs[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) xs[d][a] = (e == 0) ? u0[d][a] : Y[e >= 1 ? e - 1 : 0][d][a];
-            emit_virtual<M>(O, L, right, e, xs, Y[e], e < nR);
+            for (int d = 0; d < 3; ++d) xs[d] = (e == 0) ? u0[d] : Y[e >= 1 ? e - 1 : 0][d];
+            emit_axis<M>(O, L, right, e, a, xs, Y[e], e < nR);
         }
-#endif
     }
-    // combine the pair's flags
-    const bool spd_pair = spd && (pair_swap(spd ? 1.0 : 0.0) != 0.0);
+    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
     if (!spd_pair) return TGMS_ERR_SINGULAR;
@@ -547,16 +875,99 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
     return TGMS_OK;
 }
 
+// Whole solve of one group (single-buffered kernels).
+template <int M, bool HAS_ED>
+__device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, bool valid,
+                                              const double* __restrict__ ed, const OutCtx& O) {
+    if constexpr (M <= 2) {
+        double u0[3][3], uM[3][3];
+        const double sg = right ? -1.0 : 1.0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
+                const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
+                const double f = (d == 1) ? 1.0 : sg;
+                u0[d][a] = right ? f * s1 : s0;
+                uM[d][a] = right ? f * s0 : s1;
+            }
+        bool spd = true;
+        double fin = 0.0;
+        if constexpr (M == 1) {
+            emit_virtual<M>(O, L, right, 0, u0, uM, false);
+        } else {
+            // one interior knot: virtual knot 1 on both lanes (physical 1 for both)
+            double pp[8], pn[8], y[3][3], x[3][3];
+            rpowers(L.r(0), pp);
+            rpowers(L.r(1), pn);
+            const Sym3 D = knot_diag(pp, pn);
+            knot_rhs<HAS_ED>(L, 1, pp, pn, u0, y);
+            if (HAS_ED) {  // final derivatives through C_1 (virtual segment 1)
+                double C1[3][3];
+                coupling(pn, C1);
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        y[d][a] -= C1[d][0] * uM[0][a] + C1[d][1] * uM[1][a] + C1[d][2] * uM[2][a];
+            }
+            const Ldl3 f = ldl3s(D, spd);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                ldl3_solve(f, y[0][a], y[1][a], y[2][a], x[0][a], x[1][a], x[2][a]);
+                fin += (x[0][a] + x[1][a]) + x[2][a];
+            }
+            emit_virtual<M>(O, L, right, 0, u0, x, true);
+        }
+        const bool spd_pair = spd && (pair_swap(spd ? 1.0 : 0.0) != 0.0);
+        const double fin_pair = fin + pair_swap(fin);
+        if (!valid) return TGMS_ERR_INVALID_ARG;
+        if (!spd_pair) return TGMS_ERR_SINGULAR;
+        if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
+        return TGMS_OK;
+    } else {
+#ifndef TGMS_JOINT_AXES
+        return pair_solve_ax<M, HAS_ED>(L, right, valid, ed, O);
+#endif
+        using CH = Chain<M>;
+        PairState<M> S;
+        ps_init<M, HAS_ED>(S, L, right, valid, ed);
+#ifdef TGMS_ABL_NOCOMPUTE  // ablation: staging + emission only, knot derivatives = 0
+#pragma unroll
+        for (int s = 0; s <= CH::NS; ++s)
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) S.Y[s][d][a] = 0.0;
+#else
+        MARK(chain);
+#pragma unroll
+        for (int s = 0; s < CH::NS; ++s) {
+            SCHED_FENCE();
+            ps_chain_step<M, HAS_ED>(S, L, right, s);
+        }
+        ps_finish<M>(S, L, right);
+#endif
+#pragma unroll
+        for (int e = 0; e < CH::NE; ++e) {
+            SCHED_FENCE();
+            ps_emit_step<M>(S, O, L, right, e);
+        }
+        return ps_status<M>(S, valid);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Staging.
 
 template <int M>
-__device__ __forceinline__ void stage_row_w(Stage<M>& sm, int t, int q, double v) {
+__device__ __forceinline__ void stage_row_w(In<M>& sm, int t, int q, double v) {
     sm.W[q * PSTRIDE + t] = v;
     if (!finite(v)) atomicOr(&sm.bad[t], 1);
 }
 template <int M>
-__device__ __forceinline__ void stage_row_t(Stage<M>& sm, int t, int q, double v) {
+__device__ __forceinline__ void stage_row_t(In<M>& sm, int t, int q, double v) {
     sm.T[q * PSTRIDE + t] = v;
     sm.R[q * PSTRIDE + t] = fast_rcp(v);
     if (!finite_pos(v)) atomicOr(&sm.bad[t], 1);
@@ -565,7 +976,7 @@ __device__ __forceinline__ void stage_row_t(Stage<M>& sm, int t, int q, double v
 // Invalid trajectories are replaced by an all-zero, unit-time one (whose solution
 // is exactly zero), so the solver needs no per-coefficient masking.  Rare path.
 template <int M>
-__device__ __forceinline__ void sanitize(Stage<M>& sm, int lane) {
+__device__ __forceinline__ void sanitize(In<M>& sm, int lane) {
     if (lane < TPW && sm.bad[lane]) {
         for (int q = 0; q < (M + 1) * 3; ++q) sm.W[q * PSTRIDE + lane] = 0.0;
         for (int q = 0; q < M; ++q) {
@@ -575,92 +986,307 @@ __device__ __forceinline__ void sanitize(Stage<M>& sm, int lane) {
     }
 }
 
+// A uniform group's inputs in registers: its 32 trajectories are one contiguous
+// HBM block, read with 16-B loads across the wave.  The loads are unconditional
+// (no divergent paths, so their registers can stay in flight across other work):
+// indices are clamped into the array, and the one double a clamped pair can miss
+// (the array's last, when its length is odd) is read separately.
+template <int M>
+struct Loads {
+    static constexpr int NW = (M + 1) * 3;
+    static constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 loads per lane, waypoints
+    static constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 loads per lane, times
+    double2 wv[NW2], tv[NT2];
+    double wlast, tlast;
+};
+
+template <int M>
+__device__ __forceinline__ void issue_loads(Loads<M>& R, const double* __restrict__ W, const double* __restrict__ T,
+                                            int32_t B, int64_t b0, int lane) {
+#ifndef TGMS_ABL_NOLOAD  // ablation: skip the input loads
+    using LD = Loads<M>;
+    const int64_t nW = (int64_t)B * LD::NW, nT = (int64_t)B * M;  // doubles in the arrays
+    const int64_t jW = b0 * LD::NW / 2, jT = b0 * M / 2;          // first double2 of the group (b0 even)
+    const double2* W2 = reinterpret_cast<const double2*>(W);
+    const double2* T2 = reinterpret_cast<const double2*>(T);
+#pragma unroll
+    for (int i = 0; i < LD::NW2; ++i) {
+        const int64_t j = jW + lane + W64 * i;
+        R.wv[i] = W2[j < nW / 2 ? j : nW / 2 - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < LD::NT2; ++i) {
+        const int64_t j = jT + lane + W64 * i;
+        R.tv[i] = T2[j < nT / 2 ? j : nT / 2 - 1];
+    }
+    R.wlast = W[nW - 1];
+    R.tlast = T[nT - 1];
+#endif
+}
+
+// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left open (gfx9 encoding), as a real
+// waitcnt instruction the compiler's wait bookkeeping sees.
+constexpr unsigned VMCNT0 = 0x0F70;
+
+// The same loads as issue_loads, but straight into LDS (LDS-DMA, no VGPRs): the
+// wave's raw 16-B pieces land lane-linearly over dst's W/T/R arrays (dst is not in
+// use yet); raw_to_regs reads them back in issue_loads' register order.
+// Issued from inline asm: the compiler does not track these loads, so it cannot
+// insert conservative vmcnt(0) waits before unrelated LDS accesses; the matching
+// wait is the explicit one at the top of raw_to_regs (asm "memory" clobbers keep
+// every LDS access to dst on the right side of both).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+template <int M>
+__device__ __forceinline__ void issue_loads_lds(In<M>& dst, const double* __restrict__ W,
+                                                const double* __restrict__ T, int32_t B, int64_t b0, int lane) {
+    using LD = Loads<M>;
+    static_assert((LD::NW2 + LD::NT2) * W64 * 16 <= sizeof(double) * ((M + 1) * 3 + 2 * M) * PSTRIDE,
+                  "raw pieces must fit over W, T and R");
+    typedef __attribute__((address_space(3))) char lds_char;
+    const uint32_t raw = (uint32_t)(uintptr_t)(lds_char*)(dst.W);  // LDS byte address
+    const int64_t nW = (int64_t)B * LD::NW, nT = (int64_t)B * M;
+    const int64_t jW = b0 * LD::NW / 2, jT = b0 * M / 2;
+    const double2* W2 = reinterpret_cast<const double2*>(W);
+    const double2* T2 = reinterpret_cast<const double2*>(T);
+#pragma unroll
+    for (int i = 0; i < LD::NW2; ++i) {
+        const int64_t j = jW + lane + W64 * i;
+        glds16(W2 + (j < nW / 2 ? j : nW / 2 - 1), raw + i * W64 * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LD::NT2; ++i) {
+        const int64_t j = jT + lane + W64 * i;
+        glds16(T2 + (j < nT / 2 ? j : nT / 2 - 1), raw + (LD::NW2 + i) * W64 * 16);
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void raw_to_regs(const In<M>& src, Loads<M>& R, int lane) {
+    using LD = Loads<M>;
+    const double2* raw = reinterpret_cast<const double2*>(src.W);
+    // the LDS-DMA pieces have landed (an asm wait: the compiler does not know about
+    // the asm loads and would drop a builtin wait as redundant)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < LD::NW2; ++i) R.wv[i] = raw[i * W64 + lane];
+#pragma unroll
+    for (int i = 0; i < LD::NT2; ++i) R.tv[i] = raw[(LD::NW2 + i) * W64 + lane];
+    wave_lds_sync();  // every piece read before staging overwrites them
+}
+
+// Transpose a group's registers into LDS [field][trajectory] and flag invalid
+// trajectories (non-finite waypoint, T <= 0 or non-finite): only a wave that sees
+// one takes the LDS-atomic path and sanitises.
+template <int M>
+__device__ __forceinline__ void stage_loads(In<M>& sm, const Loads<M>& R, int32_t B, int64_t b0, int nb, int lane) {
+    using LD = Loads<M>;
+    const int nw = nb * LD::NW, nt = nb * M;  // doubles present in this group
+    const int64_t oddW = ((int64_t)B * LD::NW) & 1 ? (int64_t)B * LD::NW - 1 - b0 * LD::NW : -1;  // group-local
+    const int64_t oddT = ((int64_t)B * M) & 1 ? (int64_t)B * M - 1 - b0 * M : -1;
+    if (lane < TPW) sm.base[lane] = (b0 + lane) * (24 * M);
+    bool bad = false;
+#ifndef TGMS_ABL_NOLOAD
+    auto put_w = [&](int e, double v) {
+        if (e < nw) {
+            v = (e == oddW) ? R.wlast : v;
+            const int t = e / LD::NW, q = e - t * LD::NW;
+            sm.W[q * PSTRIDE + t] = v;
+            bad = bad || !finite(v);
+        }
+    };
+    auto put_t = [&](int e, double v) {
+        if (e < nt) {
+            v = (e == oddT) ? R.tlast : v;
+            const int t = e / M, q = e - t * M;
+            sm.T[q * PSTRIDE + t] = v;
+            sm.R[q * PSTRIDE + t] = fast_rcp(v);
+            bad = bad || !finite_pos(v);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < LD::NW2; ++i) {
+        const int e = 2 * (lane + W64 * i);
+        put_w(e, R.wv[i].x);
+        put_w(e + 1, R.wv[i].y);
+    }
+#pragma unroll
+    for (int i = 0; i < LD::NT2; ++i) {
+        const int e = 2 * (lane + W64 * i);
+        put_t(e, R.tv[i].x);
+        put_t(e + 1, R.tv[i].y);
+    }
+#endif
+    if (lane < TPW) sm.bad[lane] = 0;
+    wave_lds_sync();
+    if (__builtin_amdgcn_ballot_w64(bad) != 0) {  // rare: find the trajectories and sanitise them
+        for (int e = lane; e < nw; e += W64) {
+            const int t = e / LD::NW, q = e - t * LD::NW;
+            if (!finite(sm.W[q * PSTRIDE + t])) atomicOr(&sm.bad[t], 1);
+        }
+        for (int e = lane; e < nt; e += W64) {
+            const int t = e / M, q = e - t * M;
+            if (!finite_pos(sm.T[q * PSTRIDE + t])) atomicOr(&sm.bad[t], 1);
+        }
+        wave_lds_sync();
+        sanitize(sm, lane);
+        wave_lds_sync();
+    }
+}
+
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_MIN_WAVES) void k_reduced_uniform(int32_t B, const double* __restrict__ W,
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B, const double* __restrict__ W,
                                                                         const double* __restrict__ T,
                                                                         const double* __restrict__ ED,
                                                                         double* __restrict__ C,
                                                                         int32_t* __restrict__ status) {
-    constexpr int NW = (M + 1) * 3;
     __shared__ Stage<M> sm;
+    STAMP_RT(6);
+    STAMP(0);
     const int lane = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * TPW;
     const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
-    if (lane < TPW) {
-        sm.bad[lane] = 0;
-        sm.base[lane] = (b0 + lane) * (24 * M);
-    }
-    __syncthreads();
-#ifndef TGMS_ABL_NOLOAD  // ablation: skip the input loads (LDS holds garbage)
-    // The wave's trajectories are contiguous in HBM: 16-B loads across the wave, all
-    // issued before the first use (one memory round trip), then transposed into LDS.
-    constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 loads per lane, waypoints
-    constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 loads per lane, times
-    const double2* gW2 = reinterpret_cast<const double2*>(W + b0 * NW);
-    const double2* gT2 = reinterpret_cast<const double2*>(T + b0 * M);
-    const int nw = nb * NW, nt = nb * M;  // doubles present in this wave's block
-    double2 wv[NW2], tv[NT2];
-    if (nb == TPW) {
-#pragma unroll
-        for (int i = 0; i < NW2; ++i)
-            if ((TPW * NW) % 128 == 0 || 2 * (lane + W64 * i) < TPW * NW) wv[i] = gW2[lane + W64 * i];
-#pragma unroll
-        for (int i = 0; i < NT2; ++i)
-            if ((TPW * M) % 128 == 0 || 2 * (lane + W64 * i) < TPW * M) tv[i] = gT2[lane + W64 * i];
-    } else {  // tail block: element-wise bounds
-        const double* gW = W + b0 * NW;
-        const double* gT = T + b0 * M;
-#pragma unroll
-        for (int i = 0; i < NW2; ++i) {
-            const int e = 2 * (lane + W64 * i);
-            wv[i].x = (e < nw) ? gW[e] : 0.0;
-            wv[i].y = (e + 1 < nw) ? gW[e + 1] : 0.0;
-        }
-#pragma unroll
-        for (int i = 0; i < NT2; ++i) {
-            const int e = 2 * (lane + W64 * i);
-            tv[i].x = (e < nt) ? gT[e] : 1.0;
-            tv[i].y = (e + 1 < nt) ? gT[e + 1] : 1.0;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NW2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        if (e < nw) {
-            const int t0 = e / NW, q0 = e - t0 * NW;
-            stage_row_w(sm, t0, q0, wv[i].x);
-            const int t1 = (e + 1) / NW, q1 = e + 1 - t1 * NW;
-            if (e + 1 < nw) stage_row_w(sm, t1, q1, wv[i].y);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NT2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        if (e < nt) {
-            stage_row_t(sm, e / M, e % M, tv[i].x);
-            if (e + 1 < nt) stage_row_t(sm, (e + 1) / M, (e + 1) % M, tv[i].y);
-        }
-    }
-#endif
-    __syncthreads();
-    sanitize(sm, lane);
-    __syncthreads();
+    Loads<M> R;
+    issue_loads<M>(R, W, T, B, b0, lane);
+    stage_loads<M>(sm.in, R, B, b0, nb, lane);
+    STAMP(1);
     // Every lane runs to the end (the output stage needs the whole wave); pairs
     // beyond nb compute on stale LDS and store nothing.
     const int slot = lane >> 1;
     const bool right = lane & 1;
     const bool live = slot < nb;
     const int64_t b = b0 + slot;
-    const bool valid = sm.bad[slot] == 0;
-    const LaneView L = make_view<M>(sm, slot, right);
-    const OutCtx O = make_out(sm.O, sm.base, C, nb, lane);
+    const bool valid = sm.in.bad[slot] == 0;
+    const LaneView L = make_view<M>(sm.in, slot, right);
+    const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
     const int32_t st = pair_solve<M, HAS_ED>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    STAMP(5);
+    STAMP_RT(7);
     if (live && !right && status) status[b] = st;
+}
+
+// Two groups per wavefront, software-pipelined: the second group's loads are in
+// flight during the first group's chain, and the second group's chain runs between
+// the first group's emission steps, so the coefficient stores of one group drain
+// while the other is being solved (one wave per SIMD cannot hide either otherwise).
+// Wave w solves groups w and w + gridDim.x.
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, 1) void k_reduced_pipe(int32_t B, const double* __restrict__ W,
+                                                         const double* __restrict__ T,
+                                                         const double* __restrict__ ED, double* __restrict__ C,
+                                                         int32_t* __restrict__ status) {
+    using CH = Chain<M>;
+    // separate LDS objects, so the compiler can tell B's in-flight LDS-DMA from
+    // every access to A's inputs and to the output stage (no false vmcnt waits)
+    __shared__ alignas(16) double stageO[W64 * OSTRIDE];
+    __shared__ In<M> inA;
+    __shared__ In<M> inB;
+    STAMP_RT(6);
+    STAMP(0);
+    const int lane = threadIdx.x;
+    const int slot = lane >> 1;
+    const bool right = lane & 1;
+    const int64_t ngroups = ((int64_t)B + TPW - 1) / TPW;
+    const int64_t gA = blockIdx.x, gB = gA + gridDim.x;
+    const bool twoB = gB < ngroups;  // wave-uniform
+    const int64_t bA0 = gA * TPW, bB0 = gB * TPW;
+    const int nbA = (int)((B - bA0) < TPW ? (B - bA0) : TPW);
+    const int nbB = twoB ? (int)((B - bB0) < TPW ? (B - bB0) : TPW) : 0;
+
+    Loads<M> RA, RB;
+    issue_loads<M>(RA, W, T, B, bA0, lane);
+    SCHED_FENCE();
+    stage_loads<M>(inA, RA, B, bA0, nbA, lane);
+    // retire every load of A (some are consumed on one path only), so no later
+    // register reuse makes the compiler wait for B's in-flight LDS-DMA
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+    SCHED_FENCE();
+    // B's inputs land in LDS while A is being solved
+    if (twoB) issue_loads_lds<M>(inB, W, T, B, bB0, lane);
+    RB.wlast = RA.wlast;  // array-wide values (the arrays' last doubles)
+    RB.tlast = RA.tlast;
+    STAMP(1);
+
+    // ---- group A: chain + interface + back substitution ----
+    const bool liveA = slot < nbA;
+    const int64_t bA = bA0 + slot;
+    const bool validA = inA.bad[slot] == 0;
+    const LaneView LA = make_view<M>(inA, slot, right);
+    PairState<M> SA;
+    ps_init<M, HAS_ED>(SA, LA, right, validA, (HAS_ED && liveA) ? ED + bA * 18 : ED);
+#pragma unroll
+    for (int s = 0; s < CH::NS; ++s) {
+        SCHED_FENCE();
+        ps_chain_step<M, HAS_ED>(SA, LA, right, s);
+    }
+    ps_finish<M>(SA, LA, right);
+    {
+        const int32_t st = ps_status<M>(SA, validA);
+        if (liveA && !right && status) status[bA] = st;
+    }
+    const OutCtx OA = make_out(stageO, inA.base, C, nbA, lane);
+
+    if (twoB) {
+        SCHED_FENCE();
+        raw_to_regs<M>(inB, RB, lane);
+        stage_loads<M>(inB, RB, B, bB0, nbB, lane);
+        const bool liveB = slot < nbB;
+        const int64_t bB = bB0 + slot;
+        const bool validB = inB.bad[slot] == 0;
+        const LaneView LB = make_view<M>(inB, slot, right);
+        PairState<M> SB;
+        ps_init<M, HAS_ED>(SB, LB, right, validB, (HAS_ED && liveB) ? ED + bB * 18 : ED);
+        // ---- emission of A interleaved with the chain of B ----
+#pragma unroll
+        for (int e = 0; e < CH::NE; ++e) {
+            SCHED_FENCE();
+#ifdef TGMS_PIPE_FINE  // one chain part after each axis of the emission step
+            ChainTmp X;
+            ps_emit_step<M>(SA, OA, LA, right, e, [&](int a) {
+                if (e < CH::NS) ps_chain_part<M, HAS_ED>(SB, X, LB, right, e, a);
+            });
+#else  // whole chain step after the emission step
+            ps_emit_step<M>(SA, OA, LA, right, e);
+            if (e < CH::NS) ps_chain_step<M, HAS_ED>(SB, LB, right, e);
+#endif
+        }
+#pragma unroll
+        for (int s = CH::NE; s < CH::NS; ++s) {
+            SCHED_FENCE();
+            ps_chain_step<M, HAS_ED>(SB, LB, right, s);
+        }
+        ps_finish<M>(SB, LB, right);
+        {
+            const int32_t st = ps_status<M>(SB, validB);
+            if (liveB && !right && status) status[bB] = st;
+        }
+        const OutCtx OB = make_out(stageO, inB.base, C, nbB, lane);
+#pragma unroll
+        for (int e = 0; e < CH::NE; ++e) {
+            SCHED_FENCE();
+            ps_emit_step<M>(SB, OB, LB, right, e);
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < CH::NE; ++e) {
+            SCHED_FENCE();
+            ps_emit_step<M>(SA, OA, LA, right, e);
+        }
+    }
+    STAMP(5);
+    STAMP_RT(7);
 }
 
 // Ragged batches: one launch per segment count M over the trajectories `perm`.
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_MIN_WAVES) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
                                                                        const int32_t* __restrict__ seg_offsets,
                                                                        const double* __restrict__ W,
                                                                        const double* __restrict__ T,
@@ -676,28 +1302,39 @@ __global__ __launch_bounds__(64, TGMS_MIN_WAVES) void k_reduced_ragged(int32_t n
     const int nb = (int)((n - i0) < TPW ? (n - i0) : TPW);
     const bool live = slot < nb;
     if (lane < TPW) {
-        sm.bad[lane] = 0;
-        sm.base[lane] = 0;
+        sm.in.bad[lane] = 0;
+        sm.in.base[lane] = 0;
     }
     __syncthreads();
     int32_t b = 0;
     if (live) {
         b = perm[i0 + slot];
         const int64_t s0 = seg_offsets[b];
-        if (!right) sm.base[slot] = s0 * 24;
+        if (!right) sm.in.base[slot] = s0 * 24;
         const double* gW = W + (s0 + b) * 3;
         // the two lanes of a pair split the trajectory's rows
-        for (int q = right; q < NW; q += 2) stage_row_w(sm, slot, q, gW[q]);
-        for (int q = right; q < M; q += 2) stage_row_t(sm, slot, q, T[s0 + q]);
+        for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
+        for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
     }
     __syncthreads();
-    sanitize(sm, lane);
+    sanitize(sm.in, lane);
     __syncthreads();
-    const bool valid = sm.bad[slot] == 0;
-    const LaneView L = make_view<M>(sm, slot, right);
-    const OutCtx O = make_out(sm.O, sm.base, C, nb, lane);
+    const bool valid = sm.in.bad[slot] == 0;
+    const LaneView L = make_view<M>(sm.in, slot, right);
+    const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
     const int32_t st = pair_solve<M, HAS_ED>(L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, O);
     if (live && !right && status) status[b] = st;
+}
+
+// The pipelined kernel needs both groups' inputs in LDS with 4 waves per CU
+// (one per SIMD): 160 KiB / 4.
+template <int M>
+constexpr bool use_pipe() {
+#ifndef TGMS_PIPE  // experiment (one wave per SIMD); the default is the 2-wave axis-sequential solve
+    return false;
+#else
+    return M >= 3 && sizeof(double) * W64 * OSTRIDE + 2 * sizeof(In<M>) <= 40 * 1024;
+#endif
 }
 
 template <int M>
@@ -705,6 +1342,14 @@ hipError_t uniform_M(int32_t B, const double* W, const double* T, const double* 
                      hipStream_t stream) {
     const unsigned grid = (unsigned)((B + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
+    if constexpr (use_pipe<M>()) {
+        const unsigned g2 = (grid + 1) / 2;
+        if (ED)
+            hipLaunchKernelGGL((k_reduced_pipe<M, true>), dim3(g2), dim3(W64), 0, stream, B, W, T, ED, C, status);
+        else
+            hipLaunchKernelGGL((k_reduced_pipe<M, false>), dim3(g2), dim3(W64), 0, stream, B, W, T, ED, C, status);
+        return hipGetLastError();
+    }
     if (ED)
         hipLaunchKernelGGL((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status);
     else
@@ -758,3 +1403,9 @@ hipError_t launch_reduced_ragged_group(int M, int32_t n, const int32_t* perm, co
 }
 
 }  // namespace tgms
+
+#ifdef TGMS_STAMPS
+extern "C" int tgms_debug_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tgms::g_stamps), sizeof(unsigned long long) * (size_t)n) == hipSuccess;
+}
+#endif
