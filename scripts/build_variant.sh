@@ -5,8 +5,10 @@ cd "$(dirname "$0")/.."
 NAME=$1; shift
 P=trajectory_generator_ros2_amd
 mkdir -p $P/lib/variants $P/build/variants
+OBJS=""
 for f in tgms_reduced tgms_dense tgms_sample tgms_capi; do
-  src=$P/csrc/$f.hip; obj=$P/build/variants/${f}_$NAME.o
+  src=$P/csrc/$f.hip; obj=$P/build/variants/${f}__$NAME.o
+  OBJS="$OBJS $obj"
   if [ "$f" = tgms_reduced ]; then
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -I$P/csrc "$@" -c $src -o $obj &
   else
@@ -14,5 +16,5 @@ for f in tgms_reduced tgms_dense tgms_sample tgms_capi; do
   fi
 done
 wait
-hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libtgms_$NAME.so $P/build/variants/*_$NAME.o
+hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/variants/libtgms_$NAME.so $OBJS
 echo $P/lib/variants/libtgms_$NAME.so

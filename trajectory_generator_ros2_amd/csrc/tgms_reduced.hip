@@ -108,11 +108,12 @@ static_assert(OSTRIDE % 2 == 0, "staged rows must keep 16-B alignment");
 // knot M-j, virtual segment i = physical segment M-1-i).
 struct LaneView {
     const double* Wb;  // &W[phys knot of virtual knot 0][axis 0][slot]
-    const double* Tb;  // &T[phys segment of virtual segment 0][slot]
+    const double* Tb;  // &T[phys segment of virtual segment 0][slot] (transposed layout only)
     const double* Rb;  // &R[...]
-    int kstep;         // +-3*PSTRIDE doubles per virtual knot
-    int sstep;         // +-PSTRIDE doubles per virtual segment
-    __device__ __forceinline__ double w(int j, int a) const { return Wb[j * kstep + a * PSTRIDE]; }
+    int kstep;         // +-3 fields per virtual knot (x the field stride)
+    int sstep;         // +-1 segment per virtual segment (x the field stride)
+    int astep;         // doubles between the axes of one knot: PSTRIDE (transposed) or 1 (raw)
+    __device__ __forceinline__ double w(int j, int a) const { return Wb[j * kstep + a * astep]; }
     __device__ __forceinline__ double t(int i) const { return Tb[i * sstep]; }
     __device__ __forceinline__ double r(int i) const { return Rb[i * sstep]; }
 };
@@ -125,6 +126,37 @@ __device__ __forceinline__ LaneView make_view(const In<M>& sm, int slot, bool ri
     L.Rb = sm.R + (right ? (M - 1) * PSTRIDE : 0) + slot;
     L.kstep = right ? -3 * PSTRIDE : 3 * PSTRIDE;
     L.sstep = right ? -PSTRIDE : PSTRIDE;
+    L.astep = PSTRIDE;
+    return L;
+}
+
+// Raw layout (uniform batches): the group's inputs exactly as they sit in HBM,
+// [trajectory][knot][axis] and [trajectory][segment], copied 16 B per lane with no
+// index arithmetic; 1/T replaces T.  Column reads across the 32 slots are
+// conflict-free for W (66-dword stride) and at most 2-way for R (20-dword stride).
+template <int M>
+struct RawIn {
+    static constexpr int NW = (M + 1) * 3;
+    double W[TPW * NW];
+    double R[TPW * M];
+    int bad[TPW];
+};
+
+template <int M>
+struct alignas(16) RawStage {
+    alignas(16) double O[W64 * OSTRIDE];
+    RawIn<M> in;
+};
+
+template <int M>
+__device__ __forceinline__ LaneView make_view_raw(const RawIn<M>& sm, int slot, bool right) {
+    LaneView L;
+    L.Wb = sm.W + slot * RawIn<M>::NW + (right ? M * 3 : 0);
+    L.Tb = nullptr;
+    L.Rb = sm.R + slot * M + (right ? M - 1 : 0);
+    L.kstep = right ? -3 : 3;
+    L.sstep = right ? -1 : 1;
+    L.astep = 1;
     return L;
 }
 
@@ -160,7 +192,11 @@ __device__ __forceinline__ OutCtx make_out(double* stage, const int64_t* base, d
 // enough.  (__syncthreads() would also fence global memory: vmcnt(0) on every
 // in-flight store.)
 __device__ __forceinline__ void wave_lds_sync() {
+#ifdef TGMS_LDS_NOWAIT  // experiment: rely on in-order DS execution within the wave
+    asm volatile("" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -196,6 +232,71 @@ __device__ __forceinline__ void stage_axis(const OutCtx& o, const double (&c)[8]
     put(2, v2);
     put(3, v3);
 }
+
+// Uniform batches: the wave's 32 trajectories are one contiguous block of C, so
+// the four pieces a lane stores sit at fixed distances (8 trajectories apart) and
+// each gets its own buffer resource over the block.  One 32-bit offset per lane
+// then addresses every store, and the resources' range check drops the pieces of
+// trajectories beyond the batch (tail group) without any branch.
+struct OutBuf {
+    double* stage;                  // LDS [W64][OSTRIDE]
+    __amdgpu_buffer_rsrc_t rs[4];   // piece q: trajectories 8q .. of the wave's block
+    uint32_t voff0;                 // byte offset of the lane's piece, emission step 0, axis 0
+    int32_t estep;                  // +-1 segment (192 B) per emission step
+    bool rt;                        // the lane's pieces were staged by odd (right) lanes
+    int lane;
+};
+
+template <int M>
+__device__ __forceinline__ OutBuf make_out_buf(double* stage, double* C, int64_t b0, int nb, int lane) {
+    constexpr int TRAJ_B = M * 24 * 8;  // bytes per trajectory
+    OutBuf o;
+    o.stage = stage;
+    o.lane = lane;
+    double* base = C + b0 * (M * 24);
+    const int block = nb * TRAJ_B;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int lim = block - q * 8 * TRAJ_B;
+        o.rs[q] = __builtin_amdgcn_make_buffer_rsrc(base + (int64_t)q * 8 * M * 24, (short)0, lim > 0 ? lim : 0,
+                                                    0x00020000);
+    }
+    o.rt = (lane >> 2) & 1;
+    o.voff0 = (uint32_t)((lane >> 3) * TRAJ_B + (o.rt ? (M - 1) * 192 : 0) + (lane & 3) * 16);
+    o.estep = o.rt ? -192 : 192;
+    return o;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Stage one axis of every lane's current segment, then store it (OutBuf version;
+// `voff` is the lane's piece offset at this emission step).
+__device__ __forceinline__ void stage_axis(const OutBuf& o, const double (&c)[8], int a, uint32_t voff,
+                                           bool has_r) {
+    wave_lds_sync();  // previous readers are done with the stage
+    double2* d = reinterpret_cast<double2*>(o.stage + o.lane * OSTRIDE);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = make_double2(c[2 * j], c[2 * j + 1]);
+    wave_lds_sync();
+    auto piece = [&](int q) {
+        const int p = o.lane + W64 * q;
+        return *reinterpret_cast<const double2*>(o.stage + (p >> 2) * OSTRIDE + (p & 3) * 2);
+    };
+    const double2 v0 = piece(0), v1 = piece(1), v2 = piece(2), v3 = piece(3);
+    const uint32_t off = (has_r || !o.rt) ? voff : 0x80000000u;  // idle odd rows: out of range
+#ifndef TGMS_ABL_NOSTORE
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), o.rs[0], off, a * 64, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), o.rs[1], off, a * 64, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v2), o.rs[2], off, a * 64, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v3), o.rs[3], off, a * 64, 0);
+#else
+    asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"(v2.x), "v"(v3.x), "v"(off));
+#endif
+}
+
+// Output address of emission step e for either output context.
+__device__ __forceinline__ uint32_t out_step(const OutBuf& o, int e) { return o.voff0 + e * o.estep; }
+__device__ __forceinline__ int out_step(const OutCtx&, int e) { return e; }
 
 // Coefficients of one physical segment (a4 layout [axis][8]) from its end data:
 // physical start knot (w0, g0) and end knot (w1, g1), g = (v, a, j) x axis.
@@ -712,38 +813,43 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
 }
 
 // Coefficients of axis a of virtual segment e (knots e, e+1 with derivatives xs, xe).
-template <int M>
-__device__ __forceinline__ void emit_axis(const OutCtx& o, const LaneView& L, bool right, int e, int a,
+template <int M, class Out>
+__device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
                                           const double (&xs)[3], const double (&xe)[3], bool has_r) {
     const double ws = L.w(e, a), we = L.w(e + 1, a);
     const double w0 = right ? we : ws, w1 = right ? ws : we;
     // the odd lane runs the segment backwards: physical start = virtual knot e+1, with P
     const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
     const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
-    const double T = L.t(e), r = L.r(e);
-    const double T2 = T * T, T3 = T2 * T;
-    const double r2 = r * r, r4 = r2 * r2, r5 = r4 * r, r6 = r4 * r2, r7 = r6 * r;
-    const double dw = w1 - w0;
-    const double h1 = T * v0, h2 = T2 * a0, h3 = T3 * j0;
-    const double h5 = T * v1, h6 = T2 * a1, h7 = T3 * j1;
-    const double d4 = 35.0 * dw - 20.0 * h1 - 5.0 * h2 - (2.0 / 3.0) * h3 - 15.0 * h5 + 2.5 * h6 - (1.0 / 6.0) * h7;
-    const double d5 = -84.0 * dw + 45.0 * h1 + 10.0 * h2 + h3 + 39.0 * h5 - 7.0 * h6 + 0.5 * h7;
-    const double d6 = 70.0 * dw - 36.0 * h1 - 7.5 * h2 - (2.0 / 3.0) * h3 - 34.0 * h5 + 6.5 * h6 - 0.5 * h7;
-    const double d7 = -20.0 * dw + 10.0 * h1 + 2.0 * h2 + (1.0 / 6.0) * h3 + 10.0 * h5 - 2.0 * h6 + (1.0 / 6.0) * h7;
-    const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), d4 * r4, d5 * r5, d6 * r6, d7 * r7};
-    stage_axis(o, c, a, e, M - 1 - e, has_r);
+    // Hermite -> monomial in r = 1/T scaled variables (no T needed):
+    //   c4 = r P4, c5 = r^2 P5, c6 = r^3 P6, c7 = r^4 P7 with P linear in
+    //   D = (w1 - w0) r^3, V = v r^2, A = a r, J = j at both ends.
+    const double r = L.r(e);
+    const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
+    const double D = (w1 - w0) * r3;
+    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
+    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
+    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
+    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
+    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+    const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
+    if constexpr (sizeof(Out) == sizeof(OutBuf) && __is_same(Out, OutBuf))
+        stage_axis(o, c, a, out_step(o, e), has_r);
+    else
+        stage_axis(o, c, a, e, M - 1 - e, has_r);
 }
 
-template <int M, bool HAS_ED>
+template <int M, bool HAS_ED, class Out>
 __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, bool valid,
-                                                 const double* __restrict__ ed, const OutCtx& O) {
+                                                 const double* __restrict__ ed, const Out& O) {
     using CH = Chain<M>;
     constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS, NE = CH::NE;
     const int nl = right ? nR : nL;
     const double sg = right ? -1.0 : 1.0;
-    MARK(chain);
+    MARK(ax_factor);
     AxFactors<M> Fa;
     ax_factor<M>(Fa, L, right);
+    MARK(ax_axisloop);
     double fin = 0.0;
 #pragma unroll 1
     for (int a = 0; a < 3; ++a) {
@@ -756,6 +862,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
         }
         // ---- forward substitution ----
+        MARK(ax_fwd);
         double Y[NS + 1][3];
         {
             double pp[8];
@@ -782,6 +889,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             }
         }
         SCHED_FENCE();
+        MARK(ax_iface);
         // ---- interface (bit-identical on both lanes, see ps_finish) ----
         double xm[3];
         {
@@ -832,6 +940,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
         }
         // ---- back substitution ----
+        MARK(ax_back);
 #pragma unroll
         for (int s = NS - 1; s >= 0; --s) {
             SCHED_FENCE();
@@ -858,15 +967,17 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             }
         }
         // ---- emission of this axis ----
+        MARK(ax_emit);
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             SCHED_FENCE();
             double xs[3];
 #pragma unroll
             for (int d = 0; d < 3; ++d) xs[d] = (e == 0) ? u0[d] : Y[e >= 1 ? e - 1 : 0][d];
-            emit_axis<M>(O, L, right, e, a, xs, Y[e], e < nR);
+            emit_axis<M, Out>(O, L, right, e, a, xs, Y[e], e < nR);
         }
     }
+    MARK(ax_end);
     const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
@@ -875,10 +986,22 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     return TGMS_OK;
 }
 
+// Emit one segment (virtual knots 0, 1 with derivatives xs, xe [derivative][axis]).
+template <int M, class Out>
+__device__ __forceinline__ void emit_all_axes(const Out& O, const LaneView& L, bool right,
+                                              const double (&xs)[3][3], const double (&xe)[3][3], bool has_r) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double s3[3] = {xs[0][a], xs[1][a], xs[2][a]};
+        const double e3[3] = {xe[0][a], xe[1][a], xe[2][a]};
+        emit_axis<M, Out>(O, L, right, 0, a, s3, e3, has_r);
+    }
+}
+
 // Whole solve of one group (single-buffered kernels).
-template <int M, bool HAS_ED>
+template <int M, bool HAS_ED, class Out>
 __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, bool valid,
-                                              const double* __restrict__ ed, const OutCtx& O) {
+                                              const double* __restrict__ ed, const Out& O) {
     if constexpr (M <= 2) {
         double u0[3][3], uM[3][3];
         const double sg = right ? -1.0 : 1.0;
@@ -895,7 +1018,7 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
         bool spd = true;
         double fin = 0.0;
         if constexpr (M == 1) {
-            emit_virtual<M>(O, L, right, 0, u0, uM, false);
+            emit_all_axes<M, Out>(O, L, right, u0, uM, false);
         } else {
             // one interior knot: virtual knot 1 on both lanes (physical 1 for both)
             double pp[8], pn[8], y[3][3], x[3][3];
@@ -918,7 +1041,7 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
                 ldl3_solve(f, y[0][a], y[1][a], y[2][a], x[0][a], x[1][a], x[2][a]);
                 fin += (x[0][a] + x[1][a]) + x[2][a];
             }
-            emit_virtual<M>(O, L, right, 0, u0, x, true);
+            emit_all_axes<M, Out>(O, L, right, u0, x, true);
         }
         const bool spd_pair = spd && (pair_swap(spd ? 1.0 : 0.0) != 0.0);
         const double fin_pair = fin + pair_swap(fin);
@@ -926,9 +1049,11 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
         if (!spd_pair) return TGMS_ERR_SINGULAR;
         if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
         return TGMS_OK;
+    } else if constexpr (!__is_same(Out, OutCtx)) {
+        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid, ed, O);
     } else {
 #ifndef TGMS_JOINT_AXES
-        return pair_solve_ax<M, HAS_ED>(L, right, valid, ed, O);
+        return pair_solve_ax<M, HAS_ED, OutCtx>(L, right, valid, ed, O);
 #endif
         using CH = Chain<M>;
         PairState<M> S;
@@ -1141,32 +1266,115 @@ __device__ __forceinline__ void stage_loads(In<M>& sm, const Loads<M>& R, int32_
     }
 }
 
+// Stage a uniform group into the raw layout: 16-B loads (indices clamped into the
+// arrays, so no lane branches), copied lane-linearly to LDS; 1/T computed in
+// registers.  Returns (wave-uniform) whether any trajectory of the group is
+// invalid; only then are per-trajectory flags built and the bad ones sanitised
+// (all-zero waypoints, unit times), which a slow path re-reads from HBM.
+template <int M>
+__device__ __forceinline__ bool stage_raw(RawIn<M>& sm, const double* __restrict__ W, const double* __restrict__ T,
+                                          int32_t B, int64_t b0, int nb, int lane) {
+    constexpr int NW = RawIn<M>::NW;
+    constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 per lane, waypoints
+    constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 per lane, times
+    const int64_t nW = (int64_t)B * NW, nT = (int64_t)B * M;
+    const int64_t jW = b0 * NW / 2, jT = b0 * M / 2;  // first double2 of the group (b0 is even)
+    const int64_t mW = nW / 2 - 1 - jW, mT = nT / 2 - 1 - jT;
+    const int jmaxW = mW < (1 << 30) ? (int)mW : (1 << 30);  // last double2 inside the arrays
+    const int jmaxT = mT < (1 << 30) ? (int)mT : (1 << 30);
+    const double2* gW = reinterpret_cast<const double2*>(W) + jW;
+    const double2* gT = reinterpret_cast<const double2*>(T) + jT;
+    double2 wv[NW2], tv[NT2];
+#ifndef TGMS_ABL_NOLOAD
+#pragma unroll
+    for (int i = 0; i < NW2; ++i) {
+        const int j = lane + W64 * i;
+        wv[i] = gW[j < jmaxW ? j : jmaxW];
+    }
+#pragma unroll
+    for (int i = 0; i < NT2; ++i) {
+        const int j = lane + W64 * i;
+        tv[i] = gT[j < jmaxT ? j : jmaxT];
+    }
+#else
+#pragma unroll
+    for (int i = 0; i < NW2; ++i) wv[i] = make_double2(lane, i);
+#pragma unroll
+    for (int i = 0; i < NT2; ++i) tv[i] = make_double2(1.0 + lane, 2.0);
+#endif
+    const int nw = nb * NW, nt = nb * M;  // doubles of the group's live trajectories
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < NW2; ++i) {
+        const int e = 2 * (lane + W64 * i);
+        if ((TPW * NW) % (2 * W64) == 0 || e < TPW * NW) {
+            *reinterpret_cast<double2*>(sm.W + e) = wv[i];
+            bad = bad || (e < nw && !finite(wv[i].x)) || (e + 1 < nw && !finite(wv[i].y));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NT2; ++i) {
+        const int e = 2 * (lane + W64 * i);
+        if ((TPW * M) % (2 * W64) == 0 || e < TPW * M) {
+            *reinterpret_cast<double2*>(sm.R + e) = make_double2(fast_rcp(tv[i].x), fast_rcp(tv[i].y));
+            bad = bad || (e < nt && !finite_pos(tv[i].x)) || (e + 1 < nt && !finite_pos(tv[i].y));
+        }
+    }
+    // an array of odd length: its last double is outside every clamped pair
+    const bool oddW = (nW & 1) && (b0 + nb == B), oddT = (nT & 1) && (b0 + nb == B);
+    if (oddW || oddT) {  // tail group only (uniform branch)
+        const double wl = W[nW - 1], tl = T[nT - 1];
+        if (lane == 0) {
+            if (oddW) sm.W[nw - 1] = wl;
+            if (oddT) sm.R[nt - 1] = fast_rcp(tl);
+        }
+        bad = bad || (oddW && !finite(wl)) || (oddT && !finite_pos(tl));
+    }
+    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if (any_bad) {  // rare: per-trajectory flags from HBM, then sanitise
+        if (lane < TPW) {
+            int f = 0;
+            if (lane < nb) {
+                const double* w = W + (b0 + lane) * NW;
+                const double* t = T + (b0 + lane) * M;
+                for (int q = 0; q < NW; ++q) f |= !finite(w[q]);
+                for (int q = 0; q < M; ++q) f |= !finite_pos(t[q]);
+            }
+            sm.bad[lane] = f;
+            if (f) {
+                for (int q = 0; q < NW; ++q) sm.W[lane * NW + q] = 0.0;
+                for (int q = 0; q < M; ++q) sm.R[lane * M + q] = 1.0;
+            }
+        }
+    }
+    wave_lds_sync();
+    return any_bad;
+}
+
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B, const double* __restrict__ W,
                                                                         const double* __restrict__ T,
                                                                         const double* __restrict__ ED,
                                                                         double* __restrict__ C,
                                                                         int32_t* __restrict__ status) {
-    __shared__ Stage<M> sm;
+    __shared__ RawStage<M> sm;
     STAMP_RT(6);
     STAMP(0);
     const int lane = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * TPW;
     const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
-    Loads<M> R;
-    issue_loads<M>(R, W, T, B, b0, lane);
-    stage_loads<M>(sm.in, R, B, b0, nb, lane);
+    const bool any_bad = stage_raw<M>(sm.in, W, T, B, b0, nb, lane);
     STAMP(1);
     // Every lane runs to the end (the output stage needs the whole wave); pairs
-    // beyond nb compute on stale LDS and store nothing.
+    // beyond nb compute on stale LDS and store nothing (their buffer range is empty).
     const int slot = lane >> 1;
     const bool right = lane & 1;
     const bool live = slot < nb;
     const int64_t b = b0 + slot;
-    const bool valid = sm.in.bad[slot] == 0;
-    const LaneView L = make_view<M>(sm.in, slot, right);
-    const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
-    const int32_t st = pair_solve<M, HAS_ED>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    const bool valid = !any_bad || sm.in.bad[slot] == 0;
+    const LaneView L = make_view_raw<M>(sm.in, slot, right);
+    const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane);
+    const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, O);
     STAMP(5);
     STAMP_RT(7);
     if (live && !right && status) status[b] = st;
@@ -1322,7 +1530,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n,
     const bool valid = sm.in.bad[slot] == 0;
     const LaneView L = make_view<M>(sm.in, slot, right);
     const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
-    const int32_t st = pair_solve<M, HAS_ED>(L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, O);
+    const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, O);
     if (live && !right && status) status[b] = st;
 }
 
