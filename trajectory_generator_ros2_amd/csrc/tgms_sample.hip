@@ -1,90 +1,164 @@
 // tgms_sample.hip — sampler on gfx950.
 //
-// One wavefront per trajectory (grid-stride), lanes over samples: t_k = k*dt,
-// p/v/a/j by Horner on the segment's coefficients, yaw per tgms_yaw_mode, and the
-// last sample pinned to the final waypoint (Line.cpp:80-82 convention).
+// Goal-layout p/v/a/j/psi/dpsi at t_k = k*dt per trajectory, the last sample pinned
+// to the final waypoint and end derivatives (Line.cpp:80-82 convention); yaw per
+// tgms_yaw_mode (atan2(v_y, v_x), Figure8.cpp:123).  The output (112 B per sample)
+// dominates the traffic, so the kernel is built around the store stream:
+//   - one 256-thread workgroup per trajectory (grid-stride), whose coefficients and
+//     their derivative forms (j c_j, j(j-1) c_j, ...) plus the segment start times
+//     sit in LDS, so p/v/a/j are four pure FMA Horner chains per axis;
+//   - each wavefront evaluates 64 consecutive samples, stages them in LDS, and
+//     writes the 64 x 112 B = 7 KiB run with seven fully coalesced 16-B-per-lane
+//     stores.
 #include "tgms_device.h"
 #include "tgms_internal.h"
 
 namespace tgms {
 namespace {
 
-__global__ __launch_bounds__(256) void k_sample(int32_t B, const int32_t* __restrict__ seg_offsets,
-                                                const double* __restrict__ W,
-                                                const double* __restrict__ T,
-                                                const double* __restrict__ ED,
-                                                const double* __restrict__ C, double dt,
-                                                int yaw_mode, double yaw_const,
-                                                const int64_t* __restrict__ sample_offsets,
-                                                double* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int waves_per_block = blockDim.x / W64;
-    const int64_t wave = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
-    const int64_t n_waves = (int64_t)gridDim.x * waves_per_block;
-    for (int64_t b = wave; b < B; b += n_waves) {
+constexpr int SW = 4;                  // wavefronts per workgroup
+constexpr int G = TGMS_GOAL_STRIDE;    // 14 doubles per sample
+constexpr int CH = W64 * G / 2;        // double2 per wave chunk (448)
+
+// atan2 for the heading (|v_xy| > 1e-3 guaranteed by the caller): octant
+// reduction to u in [-tan(pi/8), tan(pi/8)], then the atan series to u^43
+// (truncation < 1e-17), all in registers the caller already has free.
+__device__ __forceinline__ double atan2_f64(double y, double x) {
+    const double ax = fabs(x), ay = fabs(y);
+    const double mx = fmax(ax, ay), mn = fmin(ax, ay);
+    const double a = mn * fast_rcp(mx);                     // [0, 1]
+    const bool hi = a > 0.41421356237309503;                // tan(pi/8)
+    const double u = hi ? (a - 1.0) * fast_rcp(a + 1.0) : a;  // atan(a) = pi/4 + atan(u)
+    const double u2 = u * u;
+    double s = 1.0 / 43.0;
+#pragma unroll
+    for (int n = 20; n >= 0; --n) s = __builtin_fma(s, -u2, 1.0 / (2 * n + 1));
+    double r = u * s + (hi ? 0.78539816339744828 : 0.0);
+    r = ay > ax ? 1.5707963267948966 - r : r;
+    r = x < 0.0 ? 3.1415926535897931 - r : r;
+    return y < 0.0 ? -r : r;
+}
+
+__device__ __forceinline__ void yaw_of(int yaw_mode, double yaw_const, const double* v, const double* acc,
+                                       double& psi, double& dpsi) {
+    const double s2 = v[0] * v[0] + v[1] * v[1];
+    const bool yv = (yaw_mode == TGMS_YAW_VELOCITY) && (s2 > 1e-6);
+    const double num = v[0] * acc[1] - v[1] * acc[0];
+    psi = yv ? atan2_f64(v[1], v[0]) : yaw_const;
+    dpsi = yv ? num / s2 : 0.0;
+}
+
+__global__ __launch_bounds__(W64 * SW) void k_sample(int32_t B, const int32_t* __restrict__ seg_offsets,
+                                                      const double* __restrict__ W,
+                                                      const double* __restrict__ T,
+                                                      const double* __restrict__ ED,
+                                                      const double* __restrict__ C, double dt, int yaw_mode,
+                                                      double yaw_const,
+                                                      const int64_t* __restrict__ sample_offsets,
+                                                      double* __restrict__ out) {
+    // per (segment, axis): [derivative order k][8] = d^k/dt^k coefficient of t^(j-k) at slot j
+    __shared__ double cf[TGMS_MAX_SEGMENTS * 3 * 4 * 8];
+    __shared__ double tau[TGMS_MAX_SEGMENTS + 1];
+    __shared__ alignas(16) double stage[SW][W64 * G];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double2* st2 = reinterpret_cast<double2*>(stage[wave]);
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
         const int64_t s0 = seg_offsets[b];
         const int M = seg_offsets[b + 1] - (int32_t)s0;
         const int64_t base = sample_offsets[b];
         const int64_t ns = sample_offsets[b + 1] - base;
-        const double* tt = T + s0;
-        const double* cc = C + s0 * 24;
-        for (int64_t k = lane; k < ns - 1; k += W64) {
-            const double t = (double)k * dt;
-            double tau = 0.0;
-            int i = 0;
-            for (int q = 0; q + 1 < M; ++q) {
-                const double nt = tau + tt[q];
-                if (nt <= t) { tau = nt; i = q + 1; }
-                else break;
-            }
-            const double lt = t - tau;
-            double* o = out + (base + k) * TGMS_GOAL_STRIDE;
-            double v[3], ac[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double* c = cc + (i * 3 + a) * 8;
-                double cv[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) cv[j] = c[j];
-                double p = cv[7], dv = 7.0 * cv[7], dd = 42.0 * cv[7], jj = 210.0 * cv[7];
-#pragma unroll
-                for (int j = 6; j >= 0; --j) p = p * lt + cv[j];
-#pragma unroll
-                for (int j = 6; j >= 1; --j) dv = dv * lt + (double)j * cv[j];
-#pragma unroll
-                for (int j = 6; j >= 2; --j) dd = dd * lt + (double)(j * (j - 1)) * cv[j];
-#pragma unroll
-                for (int j = 6; j >= 3; --j) jj = jj * lt + (double)(j * (j - 1) * (j - 2)) * cv[j];
-                o[a] = p;
-                o[3 + a] = dv;
-                o[6 + a] = dd;
-                o[9 + a] = jj;
-                v[a] = dv;
-                ac[a] = dd;
-            }
-            const double s2 = v[0] * v[0] + v[1] * v[1];
-            const bool yv = (yaw_mode == TGMS_YAW_VELOCITY) && (s2 > 1e-6);
-            o[12] = yv ? atan2(v[1], v[0]) : yaw_const;
-            o[13] = yv ? (v[0] * ac[1] - v[1] * ac[0]) / s2 : 0.0;
+        __syncthreads();  // the previous trajectory's readers are done with cf / tau
+        for (int e = tid; e < M * 24; e += W64 * SW) {  // e = (segment*3 + axis)*8 + j
+            const int j = e & 7;
+            const double c = C[s0 * 24 + e];
+            double* f = cf + (e >> 3) * 32;
+            f[j] = c;
+            f[8 + j] = (double)j * c;
+            f[16 + j] = (double)(j * (j - 1)) * c;
+            f[24 + j] = (double)(j * (j - 1) * (j - 2)) * c;
         }
-        if (lane == 0 && ns >= 1) {
-            double* o = out + (base + ns - 1) * TGMS_GOAL_STRIDE;
-            const double* wl = W + (s0 + b + M) * 3;
-            const double* ed = ED ? ED + b * 18 + 9 : nullptr;
-            double v[3], ac[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                o[a] = wl[a];
-                v[a] = ed ? ed[a] : 0.0;
-                ac[a] = ed ? ed[3 + a] : 0.0;
-                o[3 + a] = v[a];
-                o[6 + a] = ac[a];
-                o[9 + a] = ed ? ed[6 + a] : 0.0;
+        if (tid < M) tau[tid + 1] = T[s0 + tid];  // all loads in flight at once
+        __syncthreads();
+        if (tid == 0) {  // prefix sums in the same order as tgms_sample_offsets / the oracle
+            double acc = 0.0;
+            tau[0] = 0.0;
+            for (int i = 1; i <= M; ++i) {
+                acc += tau[i];
+                tau[i] = acc;
             }
-            const double s2 = v[0] * v[0] + v[1] * v[1];
-            const bool yv = (yaw_mode == TGMS_YAW_VELOCITY) && (s2 > 1e-6);
-            o[12] = yv ? atan2(v[1], v[0]) : yaw_const;
-            o[13] = yv ? (v[0] * ac[1] - v[1] * ac[0]) / s2 : 0.0;
+        }
+        __syncthreads();
+        const double* wl = W + (s0 + b + M) * 3;
+        const double* edf = ED ? ED + b * 18 + 9 : nullptr;
+        // each lane's sample times only grow: carry its segment index across chunks
+        int i = 0;
+        double t_next = M > 1 ? tau[1] : 0.0, t_cur = 0.0;
+        for (int64_t k0 = (int64_t)wave * W64; k0 < ns; k0 += W64 * SW) {
+            const int64_t k = k0 + lane;
+            // each value goes to the LDS stage as soon as it exists (few live registers
+            // across the atan2 below, which keeps three waves per SIMD resident)
+            double* so = stage[wave] + lane * G;
+            double v[2], ac[2];
+#ifdef TGMS_SAMPLE_ABL_NOCOMPUTE  // ablation: store path only
+            if (false) {
+#else
+            if (k < ns - 1) {
+#endif
+                const double t = (double)k * dt;
+                while (i + 1 < M && t_next <= t) {  // same test as the oracle's scan
+                    ++i;
+                    t_cur = t_next;
+                    t_next = tau[i + 1 < M ? i + 1 : M];
+                }
+                const double lt = t - t_cur;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const double* f = cf + (i * 3 + a) * 32;
+                    double d[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        double s = f[q * 8 + 7];
+#pragma unroll
+                        for (int j = 6; j >= q; --j) s = __builtin_fma(s, lt, f[q * 8 + j]);
+                        d[q] = s;
+                    }
+                    so[a] = d[0];
+                    so[3 + a] = d[1];
+                    so[6 + a] = d[2];
+                    so[9 + a] = d[3];
+                    if (a < 2) {
+                        v[a] = d[1];
+                        ac[a] = d[2];
+                    }
+                }
+            } else {  // the pinned final sample (and lanes past the end, never stored)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const double va = edf ? edf[a] : 0.0, aa = edf ? edf[3 + a] : 0.0;
+                    so[a] = wl[a];
+                    so[3 + a] = va;
+                    so[6 + a] = aa;
+                    so[9 + a] = edf ? edf[6 + a] : 0.0;
+                    if (a < 2) {
+                        v[a] = va;
+                        ac[a] = aa;
+                    }
+                }
+            }
+#ifndef TGMS_SAMPLE_ABL_NOCOMPUTE
+            yaw_of(yaw_mode, yaw_const, v, ac, so[12], so[13]);
+#endif
+            // 7 coalesced 16-B stores per lane of the wave's 64 staged samples
+            __builtin_amdgcn_wave_barrier();
+            const int64_t n2 = (ns - k0) * (G / 2);  // double2 of this chunk inside the trajectory
+            double2* dst = reinterpret_cast<double2*>(out + (base + k0) * G);
+#pragma unroll
+            for (int q = 0; q < G / 2; ++q) {
+                const int idx = q * W64 + lane;
+                if (idx < n2) dst[idx] = st2[idx];
+            }
+            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -96,11 +170,9 @@ hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W,
                          double yaw_const, const int64_t* sample_offsets, double* out,
                          hipStream_t stream) {
     if (B <= 0) return hipSuccess;
-    const int waves = 4;
-    int64_t blocks = (B + waves - 1) / waves;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_sample, dim3((unsigned)blocks), dim3(W64 * waves), 0, stream, B, seg_offsets, W, T,
-                       ED, C, dt, yaw_mode, yaw_const, sample_offsets, out);
+    const int64_t blocks = B < 65536 ? B : 65536;
+    hipLaunchKernelGGL(k_sample, dim3((unsigned)blocks), dim3(W64 * SW), 0, stream, B, seg_offsets, W, T, ED, C,
+                       dt, yaw_mode, yaw_const, sample_offsets, out);
     return hipGetLastError();
 }
 
