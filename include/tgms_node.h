@@ -52,6 +52,10 @@ int tgms_node_inside_bounds(tgms_node* n, double xmin, double xmax, double ymin,
 int32_t tgms_node_coefficients(tgms_node* n, double* out, int32_t cap_doubles);
 /* dt = 1 / pub_freq after tgms_node_read_parameters */
 double tgms_node_dt(const tgms_node* n);
+/* waypoints [n][3] of a reference polyline shape ("M", "I", "T", "Square"), see
+ * host/factory.hpp shapeWaypoints; returns n (0: unknown shape or > cap points) */
+int32_t tgms_node_shape_waypoints(const char* shape, double cx, double cy, double orientation, double length,
+                                  double width, double z, int32_t laps, double* out, int32_t cap);
 
 #ifdef __cplusplus
 }

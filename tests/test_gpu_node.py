@@ -129,3 +129,26 @@ def test_read_parameters_rejects_overshoot():
     wl, wh = W.min(axis=0), W.max(axis=0)
     n = MinSnapNode(base_params(x_min=wl[0], x_max=wh[0], y_min=wl[1], y_max=wh[1], z_min=wl[2], z_max=wh[2]))
     assert not n.read_parameters()
+
+
+def test_smooth_M_from_reference_shape(oracle):
+    """waypoint_source "M": the reference's M corners flown as one min-snap spline
+    (SURVEY.md §8(f) rank 4), matching the oracle through the same waypoints."""
+    from trajectory_generator_ros2_amd.node import MinSnapNode, shape_waypoints
+    p = base_params(waypoint_source="M", M_length=3.0, M_width=4.0, center_x=0.0, center_y=0.0,
+                    orientation=0.2, laps=2.0, yaw_mode="velocity")
+    p.pop("seg_times")
+    p.pop("waypoints")
+    p["v_goals"] = [1.0]
+    n = MinSnapNode(p)
+    assert n.read_parameters()
+    W = shape_waypoints("M", 0.0, 0.0, 0.2, 3.0, 4.0, 1.8, 2)
+    T = np.maximum(np.linalg.norm(np.diff(W, axis=0), axis=1), 0.5)
+    R, st = oracle.solve(W, T)
+    assert st == 0 and W.shape[0] == 9
+    C = n.coefficients()
+    assert (np.abs(C - R).max(axis=(0, 2)) / np.abs(R).max(axis=(0, 2))).max() <= TOL
+    n.generate_traj()
+    G = n.goals()
+    np.testing.assert_array_equal(G[-1, :3], W[-1])
+    assert np.allclose(G[:, 2], 1.8, atol=1e-12)   # planar shape stays at alt

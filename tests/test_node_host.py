@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -79,3 +80,48 @@ def test_no_cpu_fallback(node_lib):
     from trajectory_generator_ros2_amd.node import MinSnapNode
     n = MinSnapNode(base_params())
     assert not n.read_parameters()
+
+
+# Local polyline points of the reference shapes (M.cpp:20-26, I.cpp:28-35, T.cpp:28-33,
+# Square.cpp:26-43), restated for the check; the reference rotates them by
+# `orientation` about the centre (M.cpp:29-35).
+def _ref_shape(shape, cx, cy, th, l, w, z):
+    pts = {"M": [(-w / 2, -l / 2), (-w / 2, l / 2), (0, -l / 2), (w / 2, l / 2), (w / 2, -l / 2)],
+           "I": [(-w / 2, l / 2), (w / 2, l / 2), (0, l / 2), (0, -l / 2), (-w / 2, -l / 2), (w / 2, -l / 2)],
+           "T": [(-w / 2, l / 2), (w / 2, l / 2), (0, l / 2), (0, -l / 2)],
+           "Square": [(-l / 2, l / 2), (l / 2, l / 2), (l / 2, -l / 2), (-l / 2, -l / 2), (-l / 2, l / 2)]}[shape]
+    c, s = np.cos(th), np.sin(th)
+    return np.array([[c * x - s * y + cx, s * x + c * y + cy, z] for x, y in pts])
+
+
+@pytest.mark.parametrize("shape", ["M", "I", "T", "Square"])
+def test_shape_waypoints_match_reference_geometry(node_lib, shape):
+    from trajectory_generator_ros2_amd.node import shape_waypoints
+    got = shape_waypoints(shape, 0.5, -1.0, 0.3, 3.0, 4.0, 1.8)
+    np.testing.assert_allclose(got, _ref_shape(shape, 0.5, -1.0, 0.3, 3.0, 4.0, 1.8), rtol=0, atol=1e-12)
+
+
+def test_shape_laps_alternate_direction(node_lib):
+    from trajectory_generator_ros2_amd.node import shape_waypoints
+    one = shape_waypoints("T", length=3.0, width=4.0, z=1.0)
+    three = shape_waypoints("T", length=3.0, width=4.0, z=1.0, laps=3)
+    np.testing.assert_array_equal(three, np.concatenate([one, one[::-1][1:], one[1:]]))
+    sq2 = shape_waypoints("Square", length=2.0, z=1.0, laps=2)
+    sq1 = shape_waypoints("Square", length=2.0, z=1.0)
+    np.testing.assert_array_equal(sq2, np.concatenate([sq1, sq1[1:]]))
+    assert shape_waypoints("M", laps=5).shape[0] == 0   # 21 points > 17
+    assert shape_waypoints("Hexagon").shape[0] == 0
+
+
+@pytest.mark.parametrize("override", [
+    {"waypoint_source": "M", "M_length": 3.0},           # missing M_width
+    {"waypoint_source": "M", "M_length": -3.0, "M_width": 4.0},
+    {"waypoint_source": "Hexagon"},
+    {"waypoint_source": "I", "I_length": 3.0, "I_width": 4.0, "laps": 4.0},  # 21 points
+])
+def test_shape_source_rejects(node_lib, override):
+    from trajectory_generator_ros2_amd.node import MinSnapNode
+    p = base_params(**override)
+    p.pop("seg_times")
+    p["v_goals"] = [1.0]
+    assert not MinSnapNode(p).read_parameters()

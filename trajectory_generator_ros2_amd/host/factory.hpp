@@ -25,10 +25,88 @@
 
 namespace trajectory_generator {
 
+// Waypoints of the reference's polyline primitives, so a
+// MinSnap trajectory can fly a smooth version of them.  Local (x, y) points, rotated
+// by `orientation` about (cx, cy) as those primitives do, at altitude z:
+//   "M"      M.cpp:20-26       (-w/2,-l/2) (-w/2,l/2) (0,-l/2) (w/2,l/2) (w/2,-l/2)
+//   "I"      I.cpp:28-35       (-w/2,l/2) (w/2,l/2) (0,l/2) (0,-l/2) (-w/2,-l/2) (w/2,-l/2)
+//   "T"      T.cpp:28-33       (-w/2,l/2) (w/2,l/2) (0,l/2) (0,-l/2)
+//   "Square" Square.cpp:26-43  corners (-h,h) (h,h) (h,-h) (-h,-h) with h = l/2, closed
+// `laps` traversals alternate direction like the reference's back-and-forth loop
+// (M.cpp:50-62); a closed Square simply repeats.  Returns the number of points
+// (0 for an unknown shape or more than cap).
+inline int shapeWaypoints(const std::string& shape, double cx, double cy, double orientation, double length,
+                          double width, double z, int laps, double* out, int cap) {
+    std::vector<std::pair<double, double>> pts;
+    const double l = length, w = width;
+    if (shape == "M")
+        pts = {{-w / 2, -l / 2}, {-w / 2, l / 2}, {0.0, -l / 2}, {w / 2, l / 2}, {w / 2, -l / 2}};
+    else if (shape == "I")
+        pts = {{-w / 2, l / 2}, {w / 2, l / 2}, {0.0, l / 2}, {0.0, -l / 2}, {-w / 2, -l / 2}, {w / 2, -l / 2}};
+    else if (shape == "T")
+        pts = {{-w / 2, l / 2}, {w / 2, l / 2}, {0.0, l / 2}, {0.0, -l / 2}};
+    else if (shape == "Square")
+        pts = {{-l / 2, l / 2}, {l / 2, l / 2}, {l / 2, -l / 2}, {-l / 2, -l / 2}, {-l / 2, l / 2}};
+    else
+        return 0;
+    if (laps < 1) return 0;
+    const bool closed = shape == "Square";
+    std::vector<std::pair<double, double>> path = pts;
+    for (int lap = 1; lap < laps; ++lap) {
+        if (closed) {
+            path.insert(path.end(), pts.begin() + 1, pts.end());
+        } else {  // reverse direction each lap, sharing the turning point
+            const bool rev = lap & 1;
+            for (size_t i = 1; i < pts.size(); ++i) path.push_back(rev ? pts[pts.size() - 1 - i] : pts[i]);
+        }
+    }
+    if ((int)path.size() > cap) return 0;
+    const double c = std::cos(orientation), s = std::sin(orientation);
+    for (size_t i = 0; i < path.size(); ++i) {
+        const double x = path[i].first, y = path[i].second;
+        out[3 * i] = c * x - s * y + cx;
+        out[3 * i + 1] = s * x + c * y + cy;
+        out[3 * i + 2] = z;
+    }
+    return (int)path.size();
+}
+
 template <class Node>
 bool readMinSnapParameters(Node& node, double dt, std::unique_ptr<Trajectory>& traj) {
     MinSnapParams p;
-    if (!node.get_parameter("waypoints", p.waypoints)) return false;
+    std::string source = "list";
+    node.get_parameter("waypoint_source", source);
+    if (source != "list") {
+        // shape parameters named as in config/default.yaml (M_length, I_width, side_length, ...)
+        double cx = 0, cy = 0, orientation = 0, alt = 0, length = 0, width = 0, laps = 1;
+        if (!node.get_parameter("alt", alt)) return false;
+        node.get_parameter("center_x", cx);
+        node.get_parameter("center_y", cy);
+        node.get_parameter("orientation", orientation);
+        node.get_parameter("laps", laps);
+        if (source == "Square") {
+            if (!node.get_parameter("side_length", length)) return false;
+            width = length;
+        } else {
+            if (!node.get_parameter(source + "_length", length)) return false;
+            if (!node.get_parameter(source + "_width", width)) return false;
+        }
+        if (!(length > 0) || !(width > 0)) {
+            log_error("%s dimensions must be > 0", source.c_str());
+            return false;
+        }
+        double buf[3 * (TGMS_MAX_SEGMENTS + 1)];
+        const int n = shapeWaypoints(source, cx, cy, orientation, length, width, alt, (int)laps, buf,
+                                     TGMS_MAX_SEGMENTS + 1);
+        if (n < 2) {
+            log_error("waypoint_source %s with %d laps is not available (at most %d segments)", source.c_str(),
+                      (int)laps, TGMS_MAX_SEGMENTS);
+            return false;
+        }
+        p.waypoints.assign(buf, buf + 3 * n);
+    } else if (!node.get_parameter("waypoints", p.waypoints)) {
+        return false;
+    }
     if (p.waypoints.size() < 6 || p.waypoints.size() % 3 != 0) {
         log_error("waypoints must hold at least 2 x,y,z triples");
         return false;

@@ -104,4 +104,9 @@ int32_t tgms_node_coefficients(tgms_node* n, double* out, int32_t cap_doubles) {
 
 double tgms_node_dt(const tgms_node* n) { return n->settings.dt; }
 
+int32_t tgms_node_shape_waypoints(const char* shape, double cx, double cy, double orientation, double length,
+                                  double width, double z, int32_t laps, double* out, int32_t cap) {
+    return shapeWaypoints(shape, cx, cy, orientation, length, width, z, laps, out, cap);
+}
+
 }  // extern "C"

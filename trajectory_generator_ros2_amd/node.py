@@ -21,7 +21,7 @@ NODE_EXPORTS = [
     "tgms_node_read_parameters", "tgms_node_generate_traj", "tgms_node_generate_stop_traj",
     "tgms_node_pub_index", "tgms_node_goal_count", "tgms_node_goals", "tgms_node_frame_id",
     "tgms_node_index_keys", "tgms_node_index_msg", "tgms_node_inside_bounds", "tgms_node_coefficients",
-    "tgms_node_dt",
+    "tgms_node_dt", "tgms_node_shape_waypoints",
 ]
 
 _lib = None
@@ -49,6 +49,7 @@ def load():
         "tgms_node_index_keys": ([vp, vp, i32], i32), "tgms_node_index_msg": ([vp, i32], cp),
         "tgms_node_inside_bounds": ([vp, dbl, dbl, dbl, dbl, dbl, dbl], ctypes.c_int),
         "tgms_node_coefficients": ([vp, vp, i32], i32), "tgms_node_dt": ([vp], dbl),
+        "tgms_node_shape_waypoints": ([cp, dbl, dbl, dbl, dbl, dbl, dbl, i32, vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -56,6 +57,15 @@ def load():
         f.restype = res
     _lib = L
     return L
+
+
+def shape_waypoints(shape: str, cx=0.0, cy=0.0, orientation=0.0, length=1.0, width=1.0, z=0.0, laps=1):
+    """[n, 3] waypoints of a reference polyline shape (host/factory.hpp shapeWaypoints)."""
+    L = load()
+    out = np.zeros((17, 3), dtype=np.float64)
+    n = int(L.tgms_node_shape_waypoints(shape.encode(), cx, cy, orientation, length, width, z, int(laps),
+                                        out.ctypes.data, 17))
+    return out[:n]
 
 
 class MinSnapNode:
