@@ -105,6 +105,30 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
                                     const double* d_seg_times, const double* d_end_derivs,
                                     double* d_coeffs, int32_t* d_status, void* stream);
 
+/* ---- time-allocation refinement ----
+ * Minimises F(T) = sum_i J_i(T) + k_T * sum_i T_i per trajectory over its segment
+ * durations, J_i the snap cost of segment i at the min-snap solution.  One step
+ * solves, forms g_i = dJ_i/dT_i + k_T analytically (envelope theorem: knot
+ * derivatives fixed), and moves in log space:
+ *     T_i <- T_i * exp(clamp(-eta * T_i * g_i / F, -1/2, +1/2)).
+ * Trajectories whose solve fails keep their times.  Reduced method only
+ * (TGMS_ERR_UNSUPPORTED otherwise).  d_cost (nullable, [B]) receives F at the
+ * step's input times; dT_out must not alias dT. */
+tgms_status tgms_refine_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* d_waypoints,
+                                       const double* d_seg_times, const double* d_end_derivs, double k_T,
+                                       double eta, double* d_seg_times_out, double* d_cost, int32_t* d_status,
+                                       void* stream);
+tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
+                                     const int32_t* d_seg_offsets, const double* d_waypoints,
+                                     const double* d_seg_times, const double* d_end_derivs, double k_T, double eta,
+                                     double* d_seg_times_out, double* d_cost, int32_t* d_status, void* stream);
+/* Host convenience (blocking): `iters` steps from seg_times (updated in place),
+ * then F at the final times into cost (nullable) and, if coeffs is not NULL,
+ * the final solve.  Returns the worst per-trajectory status. */
+tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* seg_offsets, const double* waypoints,
+                              double* seg_times, const double* end_derivs, double k_T, double eta, int32_t iters,
+                              double* coeffs, double* cost, int32_t* status);
+
 /* ---- sampling at dt ----
  * Trajectory b yields tgms_sample_count(sum_i T_i, dt) samples: t_k = k*dt for
  * k = 0 .. n-2 and a final sample at sum_i T_i pinned exactly to the last

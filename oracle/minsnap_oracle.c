@@ -60,6 +60,19 @@ static int inputs_valid(int M, const double* W, const double* T, const double* E
 }
 
 /* end derivative k (1..3) at end e (0 start, 1 final), axis a */
+/* Value and first three derivatives of one axis' monomial coefficients at t. */
+static void eval_poly_at(const double* c, double t, double out[4]) {
+    for (int k = 0; k < 4; ++k) {
+        double s = 0.0;
+        for (int j = 7; j >= k; --j) {
+            double f = 1.0;
+            for (int q = 0; q < k; ++q) f *= (double)(j - q);
+            s = s * t + f * c[j];
+        }
+        out[k] = s;
+    }
+}
+
 static double end_deriv(const double* ED, int e, int k, int a) {
     return ED ? ED[e * 9 + (k - 1) * 3 + a] : 0.0;
 }
@@ -418,6 +431,81 @@ int oracle_solve_batch(int formulation, int32_t B, const int32_t* seg_offsets,
         int st = oracle_solve(formulation, M, waypoints + 3 * ((int64_t)s0 + b), seg_times + s0,
                               end_derivs ? end_derivs + 18 * (int64_t)b : NULL,
                               coeffs + 24 * (int64_t)s0);
+        if (status) status[b] = st;
+        if (st > worst) worst = st;
+    }
+    return worst;
+}
+
+/* ----------------------------------------- time-allocation refinement */
+
+/* Snap cost of one segment and its derivative in the duration, from the segment's
+ * end data g = (w0, v0, a0, j0, w1, v1, a1, j1) per axis (KH above):
+ *   J = sum_ab KH[a][b] T^(s_a+s_b-7) g_a g_b,
+ *   dJ/dT = sum_ab KH[a][b] (s_a+s_b-7) T^(s_a+s_b-8) g_a g_b
+ * (knot data held fixed: at the optimum only the explicit T dependence counts). */
+static void segment_cost(const double* c, const double* w0, const double* w1, double T, double* J, double* dJ) {
+    double j = 0.0, dj = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double* ca = c + 8 * a;
+        double e1[4];
+        eval_poly_at(ca, T, e1);
+        const double g[8] = {w0[a], ca[1], 2.0 * ca[2], 6.0 * ca[3], w1[a], e1[1], e1[2], e1[3]};
+        for (int x = 0; x < 8; ++x)
+            for (int y = 0; y < 8; ++y) {
+                const int n = SIG[x] + SIG[y] - 7;
+                const double k = KH[x][y] * g[x] * g[y];
+                j += k * pow(T, n);
+                dj += k * n * pow(T, n - 1);
+            }
+    }
+    *J = j;
+    *dJ = dj;
+}
+
+int oracle_refine_times(int formulation, int M, const double* W, double* T, const double* ED, double kT,
+                        double eta, int iters, double* cost, double* C) {
+    double buf[24 * ORACLE_MAX_SEGMENTS];
+    double* c = C ? C : buf;
+    if (!W || !T || !inputs_valid(M, W, T, ED)) return ORACLE_INVALID;
+    for (int it = 0; it <= iters; ++it) {
+        int st = oracle_solve(formulation, M, W, T, ED, c);
+        if (st != ORACLE_OK) return st;
+        double Jv[ORACLE_MAX_SEGMENTS], dJv[ORACLE_MAX_SEGMENTS], F = 0.0;
+        for (int i = 0; i < M; ++i) {
+            segment_cost(c + 24 * i, W + 3 * i, W + 3 * (i + 1), T[i], &Jv[i], &dJv[i]);
+            F += Jv[i] + kT * T[i];
+        }
+        if (it == iters) { /* final times: report F, keep the final solve in C */
+            if (cost) *cost = F;
+            break;
+        }
+        if (!(F > 0.0)) continue;
+        for (int i = 0; i < M; ++i) {
+            double dtau = -eta * T[i] * (dJv[i] + kT) / F;
+            dtau = dtau < -0.5 ? -0.5 : (dtau > 0.5 ? 0.5 : dtau);
+            T[i] = T[i] * exp(dtau);
+        }
+    }
+    return ORACLE_OK;
+}
+
+int oracle_refine_batch(int formulation, int32_t B, const int32_t* seg_offsets, const double* waypoints,
+                        double* seg_times, const double* end_derivs, double kT, double eta, int iters,
+                        double* cost, double* coeffs, int32_t* status, int nthreads) {
+    if (B < 0 || (B > 0 && (!seg_offsets || !waypoints || !seg_times))) return ORACLE_INVALID;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+    int worst = ORACLE_OK;
+#pragma omp parallel for schedule(dynamic, 4) reduction(max : worst)
+    for (int32_t b = 0; b < B; ++b) {
+        int32_t s0 = seg_offsets[b], M = seg_offsets[b + 1] - s0;
+        int st = oracle_refine_times(formulation, M, waypoints + 3 * ((int64_t)s0 + b), seg_times + s0,
+                                     end_derivs ? end_derivs + 18 * (int64_t)b : NULL, kT, eta, iters,
+                                     cost ? cost + b : NULL, coeffs ? coeffs + 24 * (int64_t)s0 : NULL);
         if (status) status[b] = st;
         if (st > worst) worst = st;
     }

@@ -76,6 +76,18 @@ int oracle_assemble_kkt(int M, const double* waypoints, const double* seg_times,
  * final sample pinned at total_T. */
 int64_t oracle_sample_count(double total_T, double dt);
 
+/* Time-allocation refinement (the GPU step of include/tgms.h, restated): `iters`
+ * steps of  T_i <- T_i exp(clamp(-eta T_i (dJ_i/dT_i + kT) / F, -1/2, 1/2)),
+ * F = sum_i J_i + kT sum_i T_i, each after a solve with `formulation`; T is
+ * updated in place; cost (nullable) gets F at the final times and C (nullable)
+ * the final solve. */
+int oracle_refine_times(int formulation, int M, const double* waypoints, double* seg_times,
+                        const double* end_derivs, double kT, double eta, int iters, double* cost,
+                        double* coeffs);
+int oracle_refine_batch(int formulation, int32_t B, const int32_t* seg_offsets, const double* waypoints,
+                        double* seg_times, const double* end_derivs, double kT, double eta, int iters,
+                        double* cost, double* coeffs, int32_t* status, int nthreads);
+
 /* Yaw modes for sampling. */
 #define ORACLE_YAW_CONSTANT 0
 #define ORACLE_YAW_VELOCITY 1

@@ -49,6 +49,12 @@ def lib():
         L.oracle_sample.argtypes = [ctypes.c_int, dp, dp, dp, dp, ctypes.c_double, ctypes.c_int,
                                     ctypes.c_double, dp]
         L.oracle_sample.restype = ctypes.c_int64
+        L.oracle_refine_times.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_int, dp, dp]
+        L.oracle_refine_times.restype = ctypes.c_int
+        L.oracle_refine_batch.argtypes = [ctypes.c_int, ctypes.c_int32, ip, dp, dp, dp, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_int, dp, dp, ip, ctypes.c_int]
+        L.oracle_refine_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -120,3 +126,33 @@ def sample(coeffs, seg_times, waypoints, end_derivs, dt, yaw_mode=YAW_CONSTANT, 
     out = np.zeros((n + 1, 14))
     got = lib().oracle_sample(M, _dp(C), _dp(T), _dp(W), _dp(ED), dt, yaw_mode, yaw_const, _dp(out))
     return out[:got]
+
+
+def refine_times(waypoints, seg_times, end_derivs=None, k_T=1.0, eta=0.1, iters=10, formulation: int = KKT_C4):
+    """One trajectory: (refined T, final cost F, final coefficients, status)."""
+    W = np.ascontiguousarray(waypoints, dtype=np.float64)
+    T = np.array(seg_times, dtype=np.float64)
+    ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64)
+    M = T.shape[0]
+    C = np.zeros((M, 3, 8))
+    cost = np.zeros(1)
+    st = lib().oracle_refine_times(formulation, M, _dp(W), _dp(T), _dp(ED), float(k_T), float(eta), int(iters),
+                                   _dp(cost), _dp(C))
+    return T, float(cost[0]), C, st
+
+
+def refine_batch(seg_offsets, waypoints, seg_times, end_derivs=None, k_T=1.0, eta=0.1, iters=10,
+                 formulation: int = KKT_C4, nthreads: int = 0):
+    """CSR batch: (refined T [S], cost [B], coeffs [S,3,8], status [B])."""
+    so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+    W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
+    T = np.array(seg_times, dtype=np.float64).reshape(-1)
+    ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
+    B = so.shape[0] - 1
+    C = np.zeros((int(so[-1]), 3, 8))
+    cost = np.zeros(B)
+    st = np.zeros(B, dtype=np.int32)
+    lib().oracle_refine_batch(formulation, B, _ip(so), _dp(W), _dp(T), _dp(ED), float(k_T), float(eta), int(iters),
+                              _dp(cost), _dp(C), _ip(st), nthreads)
+    return T, cost, C, st
+

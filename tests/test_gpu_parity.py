@@ -240,3 +240,50 @@ def test_sharded_solve_matches_unsharded(solver):
         sts.append(st[: sb.hi - sb.lo])
     np.testing.assert_array_equal(np.concatenate(parts), C_all)
     np.testing.assert_array_equal(np.concatenate(sts), st_all[:3001])
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+def test_refine_matches_oracle(solver, oracle, ragged):
+    """Config-5 time refinement (10 steps + final solve) on the GPU vs the oracle's
+    restatement of the same step.  Ten steps of a smooth map move the fp64
+    rounding differences of the solves (~1e-11) by a small factor: tolerance 1e-8."""
+    from trajectory_generator_ros2_amd import synthetic as S
+    if ragged:
+        so, W, T = S.ragged_batch(257, 1, 16, seed=21)
+    else:
+        so, W, T = S.uniform_batch(257, 10, seed=21)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+    Tg, Cg, cg, stg, worst = solver.refine(so, W, T, None, 1.0, 0.1, 10)
+    To, co, Co, sto = oracle.refine_batch(so, W, T, None, 1.0, 0.1, 10, oracle.REDUCED)
+    assert worst == 0 and (sto == 0).all()
+    assert np.abs(Tg / To - 1).max() <= 1e-8
+    assert np.abs(cg / co - 1).max() <= 1e-8
+    assert batch_rel_err(so, Cg, Co) <= 1e-8
+    assert not np.array_equal(Tg, T)
+
+
+def test_refine_device_step_and_errors(solver):
+    import torch
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_UNSUPPORTED, METHOD_DENSE_KKT, TgmsError
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(100, 7, seed=4)
+    dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+    dT2 = torch.empty_like(dT)
+    dcost = torch.empty(100, dtype=torch.float64, device="cuda")
+    solver.refine_uniform_device(100, 7, dW, dT, dT2, 1.0, 0.0, dcost)   # eta = 0: same times
+    torch.cuda.synchronize()
+    assert torch.equal(dT2, dT) and bool((dcost > 0).all())
+    with pytest.raises(TgmsError) as e:
+        solver.refine_uniform_device(100, 7, dW, dT, dT, 1.0, 0.1)       # aliasing in/out
+    assert e.value.status == ERR_INVALID_ARG
+    with pytest.raises(TgmsError) as e:
+        solver.refine_uniform_device(100, 7, dW, dT, dT2, -1.0, 0.1)     # k_T < 0
+    assert e.value.status == ERR_INVALID_ARG
+    solver.set_method(METHOD_DENSE_KKT)
+    try:
+        with pytest.raises(TgmsError) as e:
+            solver.refine_uniform_device(100, 7, dW, dT, dT2, 1.0, 0.1)
+        assert e.value.status == ERR_UNSUPPORTED
+    finally:
+        from trajectory_generator_ros2_amd import METHOD_REDUCED
+        solver.set_method(METHOD_REDUCED)

@@ -1,0 +1,78 @@
+"""CPU: the time-allocation refinement math in the oracle.
+
+There is no reference counterpart (the reference has no solver), so the step is
+pinned by its own definition:
+  - dJ_i/dT_i from the segment's end data (envelope theorem) equals a central
+    finite difference of the re-solved optimal cost J(T);
+  - the per-segment cost formula equals sum_axes c^T Q c with the survey's a1
+    Hessian Q_jk = j!/(j-4)! k!/(k-4)! T^(j+k-7)/(j+k-7);
+  - eta = 0 leaves T unchanged; steps lower F on the config-3 data."""
+import math
+
+import numpy as np
+import pytest
+
+from trajectory_generator_ros2_amd import synthetic as S
+
+
+def _cost(O, W, T, kT=0.0):
+    _, F, C, st = O.refine_times(W, T, None, kT, 0.0, 0, O.KKT_C4)
+    assert st == 0
+    return F, C
+
+
+def _q_cost(C, T):
+    """survey a1: sum over segments/axes of c^T Q(T) c."""
+    J = 0.0
+    for i, Ti in enumerate(T):
+        for a in range(3):
+            c = C[i, a]
+            for j in range(4, 8):
+                for k in range(4, 8):
+                    f = math.factorial(j) / math.factorial(j - 4) * math.factorial(k) / math.factorial(k - 4)
+                    J += c[j] * c[k] * f * Ti ** (j + k - 7) / (j + k - 7)
+    return J
+
+
+def test_cost_matches_survey_hessian(oracle):
+    _, W, T = S.uniform_batch(4, 5, seed=3)
+    for b in range(4):
+        F, C = _cost(oracle, W[b], T[b])
+        assert abs(F - _q_cost(C, T[b])) <= 1e-10 * F
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 6])
+def test_gradient_matches_finite_difference(oracle, M):
+    """One step with a tiny eta exposes g_i through T_new = T exp(-eta T g / F)."""
+    _, W, T = S.uniform_batch(3, M, seed=5)
+    kT = 0.7
+    for b in range(3):
+        F, _ = _cost(oracle, W[b], T[b], kT)
+        eta = 1e-9
+        Tn, _, _, st = oracle.refine_times(W[b], T[b], None, kT, eta, 1, oracle.KKT_C4)
+        assert st == 0
+        g = -np.log(Tn / T[b]) * F / (eta * T[b])  # analytic dF/dT_i recovered from the step
+        for i in range(M):
+            h = 1e-6 * T[b][i]
+            Tp, Tm = T[b].copy(), T[b].copy()
+            Tp[i] += h
+            Tm[i] -= h
+            fd = (_cost(oracle, W[b], Tp, kT)[0] - _cost(oracle, W[b], Tm, kT)[0]) / (2 * h)
+            assert abs(g[i] - fd) <= 1e-4 * (abs(fd) + kT), (i, g[i], fd)
+
+
+def test_eta_zero_keeps_times(oracle):
+    so, W, T = S.ragged_batch(20, 1, 8, seed=9)
+    Tn, cost, _, st = oracle.refine_batch(so, W, T, None, 1.0, 0.0, 5, oracle.REDUCED)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(Tn, T.reshape(-1))
+
+
+def test_refinement_lowers_cost(oracle):
+    so, W, T = S.uniform_batch(64, 10, seed=2)
+    _, c0, _, _ = oracle.refine_batch(so, W, T, None, 1.0, 0.1, 0, oracle.REDUCED)
+    Tn, c10, _, st = oracle.refine_batch(so, W, T, None, 1.0, 0.1, 10, oracle.REDUCED)
+    assert (st == 0).all()
+    assert (c10 <= c0 * (1 + 1e-12)).mean() > 0.95
+    assert np.median(c10 / c0) < 0.95
+    assert (Tn > 0).all()

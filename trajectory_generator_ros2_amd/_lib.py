@@ -24,6 +24,7 @@ EXPORTS = [
     "tgms_abi_version", "tgms_status_string", "tgms_create", "tgms_destroy", "tgms_last_error",
     "tgms_set_method", "tgms_solve_batch", "tgms_solve_uniform_device", "tgms_solve_batch_device",
     "tgms_sample_count", "tgms_sample_offsets", "tgms_sample_batch", "tgms_sample_batch_device",
+    "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_batch",
 ]
 
 _lib = None
@@ -78,6 +79,12 @@ def load(path: str = ""):
     L.tgms_sample_batch.restype = ctypes.c_int
     L.tgms_sample_batch_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, ctypes.c_int, dbl, vp, vp, vp]
     L.tgms_sample_batch_device.restype = ctypes.c_int
+    L.tgms_refine_uniform_device.argtypes = [vp, i32, i32, vp, vp, vp, dbl, dbl, vp, vp, vp, vp]
+    L.tgms_refine_uniform_device.restype = ctypes.c_int
+    L.tgms_refine_batch_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, vp, vp, vp, vp]
+    L.tgms_refine_batch_device.restype = ctypes.c_int
+    L.tgms_refine_batch.argtypes = [vp, i32, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp]
+    L.tgms_refine_batch.restype = ctypes.c_int
     if L.tgms_abi_version() != ABI_VERSION:
         raise ImportError(f"libtgms ABI {L.tgms_abi_version()} != {ABI_VERSION}")
     _lib = L

@@ -150,6 +150,35 @@ tgms_status dispatch(tgms_handle* h, int32_t B, int uniform_m, const std::vector
     return TGMS_OK;
 }
 
+// One refinement step over a batch (uniform or ragged), reduced method only.
+tgms_status dispatch_refine(tgms_handle* h, int32_t B, int uniform_m, const std::vector<int32_t>& counts,
+                            const int32_t* h_so, const int32_t* d_so, const double* W, const double* T,
+                            const double* ED, double kT, double eta, double* Tout, double* cost, int32_t* st,
+                            hipStream_t stream) {
+    if (B == 0) return TGMS_OK;
+    if (uniform_m > 0) {
+        TGMS_HIP(h, tgms::launch_refine_uniform(uniform_m, B, W, T, ED, kT, eta, Tout, cost, st, stream));
+        return TGMS_OK;
+    }
+    std::vector<int32_t> starts;
+    tgms_status s = upload_plan(h, B, h_so, counts, &starts, stream);
+    if (s != TGMS_OK) return s;
+    for (size_t m = 1; m < counts.size(); ++m) {
+        if (!counts[m]) continue;
+        TGMS_HIP(h, tgms::launch_refine_ragged_group((int)m, counts[m], h->d_perm + starts[m], d_so, W, T, ED, kT,
+                                                     eta, Tout, cost, st, stream));
+    }
+    return TGMS_OK;
+}
+
+tgms_status check_refine_args(tgms_handle* h, double kT, double eta) {
+    if (h->method != TGMS_METHOD_REDUCED)
+        return set_err(h, TGMS_ERR_UNSUPPORTED, "time refinement needs the reduced method");
+    if (!(kT >= 0.0) || !std::isfinite(kT) || !(eta >= 0.0) || !std::isfinite(eta))
+        return set_err(h, TGMS_ERR_INVALID_ARG, "k_T and eta must be finite and >= 0");
+    return TGMS_OK;
+}
+
 int max_m_for(const tgms_handle* h) {
     return h->method == TGMS_METHOD_DENSE_KKT ? TGMS_DENSE_MAX_SEGMENTS : TGMS_MAX_SEGMENTS;
 }
@@ -305,6 +334,107 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     return dispatch(h, B, um, counts, h_so, d_so, dW, dT, dED, dC, dSt, static_cast<hipStream_t>(stream));
+}
+
+tgms_status tgms_refine_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* dW, const double* dT,
+                                       const double* dED, double k_T, double eta, double* dT_out, double* d_cost,
+                                       int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    tgms_status s = check_refine_args(h, k_T, eta);
+    if (s != TGMS_OK) return s;
+    if (B < 0 || M < 1 || M > TGMS_MAX_SEGMENTS) return set_err(h, TGMS_ERR_INVALID_ARG, "bad B or M");
+    if (B == 0) return TGMS_OK;
+    if (!dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
+    TGMS_HIP(h, tgms::launch_refine_uniform(M, B, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
+                                            static_cast<hipStream_t>(stream)));
+    return TGMS_OK;
+}
+
+tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h_so, const int32_t* d_so,
+                                     const double* dW, const double* dT, const double* dED, double k_T, double eta,
+                                     double* dT_out, double* d_cost, int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    tgms_status s = check_refine_args(h, k_T, eta);
+    if (s != TGMS_OK) return s;
+    std::vector<int32_t> counts;
+    int um = 0;
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, &counts, &um);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!d_so || !dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
+    return dispatch_refine(h, B, um, counts, h_so, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
+                           static_cast<hipStream_t>(stream));
+}
+
+tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,
+                              double* seg_times, const double* end_derivs, double k_T, double eta, int32_t iters,
+                              double* coeffs, double* cost, int32_t* status) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    tgms_status s = check_refine_args(h, k_T, eta);
+    if (s != TGMS_OK) return s;
+    if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
+    std::vector<int32_t> counts;
+    int um = 0;
+    s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, &counts, &um);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!waypoints || !seg_times) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times");
+    TGMS_HIP(h, hipSetDevice(h->device));
+    const size_t S = (size_t)so[B];
+    const size_t nW = (S + B) * 3, nED = end_derivs ? (size_t)B * 18 : 0, nC = coeffs ? S * 24 : 0;
+    size_t off = 0;
+    const size_t oW = off; off = align256(off + nW * 8);
+    const size_t oT0 = off; off = align256(off + S * 8);
+    const size_t oT1 = off; off = align256(off + S * 8);
+    const size_t oED = off; off = align256(off + nED * 8);
+    const size_t oC = off; off = align256(off + nC * 8);
+    const size_t oCost = off; off = align256(off + (size_t)B * 8);
+    const size_t oSt = off; off = align256(off + (size_t)B * 4);
+    const size_t oSo = off; off = align256(off + (size_t)(B + 1) * 4);
+    s = ensure_ws(h, off);
+    if (s != TGMS_OK) return s;
+    char* base = static_cast<char*>(h->d_ws);
+    double* dW = reinterpret_cast<double*>(base + oW);
+    double* dT[2] = {reinterpret_cast<double*>(base + oT0), reinterpret_cast<double*>(base + oT1)};
+    double* dED = end_derivs ? reinterpret_cast<double*>(base + oED) : nullptr;
+    double* dC = reinterpret_cast<double*>(base + oC);
+    double* dCost = reinterpret_cast<double*>(base + oCost);
+    int32_t* dSt = reinterpret_cast<int32_t*>(base + oSt);
+    int32_t* dSo = reinterpret_cast<int32_t*>(base + oSo);
+    hipStream_t st = h->stream;
+    TGMS_HIP(h, hipMemcpyAsync(dW, waypoints, nW * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dT[0], seg_times, S * 8, hipMemcpyHostToDevice, st));
+    if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    int cur = 0;
+    for (int32_t k = 0; k < iters; ++k, cur ^= 1) {
+        s = dispatch_refine(h, B, um, counts, so, dSo, dW, dT[cur], dED, k_T, eta, dT[cur ^ 1], nullptr, dSt, st);
+        if (s != TGMS_OK) return s;
+    }
+    // cost at the final times (a step with eta = 0 leaves them unchanged), then the solve
+    s = dispatch_refine(h, B, um, counts, so, dSo, dW, dT[cur], dED, k_T, 0.0, dT[cur ^ 1], dCost, dSt, st);
+    if (s != TGMS_OK) return s;
+    if (coeffs) {
+        s = dispatch(h, B, um, counts, so, dSo, dW, dT[cur], dED, dC, dSt, st);
+        if (s != TGMS_OK) return s;
+        TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
+    }
+    TGMS_HIP(h, hipMemcpyAsync(seg_times, dT[cur], S * 8, hipMemcpyDeviceToHost, st));
+    if (cost) TGMS_HIP(h, hipMemcpyAsync(cost, dCost, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> hst;
+    int32_t* stout = status;
+    if (!stout) {
+        hst.resize(B);
+        stout = hst.data();
+    }
+    TGMS_HIP(h, hipMemcpyAsync(stout, dSt, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    TGMS_HIP(h, hipStreamSynchronize(st));
+    int worst = TGMS_OK;
+    for (int32_t b = 0; b < B; ++b) worst = std::max(worst, (int)stout[b]);
+    return (tgms_status)worst;
 }
 
 int64_t tgms_sample_count(double total_T, double dt) {

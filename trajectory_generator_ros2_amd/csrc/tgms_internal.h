@@ -26,7 +26,15 @@ hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nul
                             const double* T, const double* ED, double* C, int32_t* status,
                             hipStream_t stream);
 
-// Sampler: one wavefront per trajectory (grid-stride), 14 doubles per sample.
+// Time-allocation refinement step (solve + snap-cost gradient + log-space step on T):
+// uniform batches, and one M group of a ragged batch.  Tout may not alias T.
+hipError_t launch_refine_uniform(int M, int32_t B, const double* W, const double* T, const double* ED, double kT,
+                                 double eta, double* Tout, double* cost, int32_t* status, hipStream_t stream);
+hipError_t launch_refine_ragged_group(int M, int32_t n, const int32_t* perm, const int32_t* seg_offsets,
+                                      const double* W, const double* T, const double* ED, double kT, double eta,
+                                      double* Tout, double* cost, int32_t* status, hipStream_t stream);
+
+// Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,
                          const double* ED, const double* C, double dt, int yaw_mode,
                          double yaw_const, const int64_t* sample_offsets, double* out,

@@ -26,6 +26,8 @@
 // loaded with 16-B loads all in flight at once and transposed into LDS
 // ([field][trajectory], padded); coefficients leave through a 16-B-aligned LDS
 // stage so each store instruction writes whole 64-B (segment, axis) rows.
+#include <type_traits>
+
 #include "tgms_device.h"
 #include "tgms_internal.h"
 
@@ -813,6 +815,47 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
 }
 
 // Coefficients of axis a of virtual segment e (knots e, e+1 with derivatives xs, xe).
+// ---------------------------------------------------------------------------
+// Time-allocation refinement: instead of storing a
+// segment's coefficients, accumulate its snap cost J_i and dJ_i/dT_i.  With the
+// knot data held fixed (they are optimal, so by the envelope theorem only the
+// explicit dependence on T_i counts) and u = (w r^3, v r^2, a r, j) at both ends,
+//   J_i = r u^T KH u,   dJ_i/dT_i = r^2 u^T (KH o (s_a + s_b - 7)) u
+// (KH: oracle/minsnap_oracle.c, s = derivative order).  The position entries of
+// KH are antisymmetric between the ends, so only D = (w1 - w0) r^3 appears.
+template <int NE>
+struct GradAcc {
+    mutable double J[NE];   // per emission step of this lane: cost of its segment
+    mutable double dJ[NE];  // and its derivative in the segment's duration
+};
+template <class T>
+struct is_grad : std::false_type {};
+template <int NE>
+struct is_grad<GradAcc<NE>> : std::true_type {};
+
+__device__ __forceinline__ void seg_cost(double D, const double (&z)[6], double& Q, double& Qd) {
+    // z = (V0, A0, J0, V1, A1, J1); derivative orders 1,2,3,1,2,3
+    constexpr double KP[6] = {-50400, -10080, -840, -50400, 10080, -840};  // KH[4][b]
+    constexpr double KD[6][6] = {{25920, 5400, 480, 24480, -4680, 360},   {5400, 1200, 120, 4680, -840, 60},
+                                 {480, 120, 16, 360, -60, 4},             {24480, 4680, 360, 25920, -5400, 480},
+                                 {-4680, -840, -60, -5400, 1200, -120},   {360, 60, 4, 480, -120, 16}};
+    constexpr int S[6] = {1, 2, 3, 1, 2, 3};
+    double q = 100800.0 * D * D, qd = -7.0 * 100800.0 * D * D;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        double t = 2.0 * KP[a] * D, td = 2.0 * KP[a] * (S[a] - 7) * D;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            t = __builtin_fma(KD[a][b], z[b], t);
+            td = __builtin_fma(KD[a][b] * (S[a] + S[b] - 7), z[b], td);
+        }
+        q = __builtin_fma(t, z[a], q);
+        qd = __builtin_fma(td, z[a], qd);
+    }
+    Q = q;
+    Qd = qd;
+}
+
 template <int M, class Out>
 __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
                                           const double (&xs)[3], const double (&xe)[3], bool has_r) {
@@ -832,11 +875,20 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
     const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
     const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
     const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
-    const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
-    if constexpr (sizeof(Out) == sizeof(OutBuf) && __is_same(Out, OutBuf))
-        stage_axis(o, c, a, out_step(o, e), has_r);
-    else
-        stage_axis(o, c, a, e, M - 1 - e, has_r);
+    if constexpr (is_grad<Out>::value) {
+        const double z[6] = {V0, A0, j0, V1, A1, j1};
+        double Q, Qd;
+        seg_cost(D, z, Q, Qd);
+        const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
+        o.J[e] += mine ? r * Q : 0.0;
+        o.dJ[e] += mine ? r2 * Qd : 0.0;
+    } else {
+        const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
+        if constexpr (__is_same(Out, OutBuf))
+            stage_axis(o, c, a, out_step(o, e), has_r);
+        else
+            stage_axis(o, c, a, e, M - 1 - e, has_r);
+    }
 }
 
 template <int M, bool HAS_ED, class Out>
@@ -1492,6 +1544,112 @@ __global__ __launch_bounds__(64, 1) void k_reduced_pipe(int32_t B, const double*
     STAMP_RT(7);
 }
 
+// ---------------------------------------------------------------------------
+// Time-allocation refinement step: solve, then move every segment duration along
+// the normalised gradient of  F(T) = sum_i J_i(T) + k_T sum_i T_i  in log space,
+//   g_i = dJ_i/dT_i + k_T,   T_i <- T_i exp(clamp(-eta T_i g_i / F, -1/2, 1/2)),
+// (the clamp bounds one step to a factor e^(+-1/2); trajectories whose solve failed
+// keep their times).  oracle_refine_times restates the same step on the CPU.
+template <int M>
+__device__ __forceinline__ void refine_update(const GradAcc<Chain<M>::NE>& G, bool right, int32_t st, bool live,
+                                              double kT, double eta, const double* __restrict__ Tin,
+                                              double* __restrict__ Tout, double* __restrict__ cost) {
+    using CH = Chain<M>;
+    constexpr int NE = CH::NE;
+    const int nmine = right ? CH::nR : NE;
+    double Tl[NE];
+    double Fl = 0.0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int phys = right ? M - 1 - e : e;
+        const bool mine = live && e < nmine;
+        Tl[e] = mine ? Tin[phys] : 0.0;
+        Fl += mine ? G.J[e] + kT * Tl[e] : 0.0;
+    }
+    const double F = Fl + pair_swap(Fl);
+    const bool ok = (st == TGMS_OK) && F > 0.0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        if (live && e < nmine) {
+            const int phys = right ? M - 1 - e : e;
+            double dtau = -eta * Tl[e] * (G.dJ[e] + kT) / F;
+            dtau = fmin(fmax(dtau, -0.5), 0.5);
+            Tout[phys] = ok ? Tl[e] * exp(dtau) : Tl[e];
+        }
+    }
+    if (live && !right && cost) *cost = F;
+}
+
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_uniform(int32_t B, const double* __restrict__ W,
+                                                                       const double* __restrict__ T,
+                                                                       const double* __restrict__ ED, double kT,
+                                                                       double eta, double* __restrict__ Tout,
+                                                                       double* __restrict__ cost,
+                                                                       int32_t* __restrict__ status) {
+    __shared__ RawIn<M> sm;
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * TPW;
+    const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
+    const bool any_bad = stage_raw<M>(sm, W, T, B, b0, nb, lane);
+    const int slot = lane >> 1;
+    const bool right = lane & 1;
+    const bool live = slot < nb;
+    const int64_t b = b0 + slot;
+    const bool valid = !any_bad || sm.bad[slot] == 0;
+    const LaneView L = make_view_raw<M>(sm, slot, right);
+    GradAcc<Chain<M>::NE> G;
+#pragma unroll
+    for (int e = 0; e < Chain<M>::NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+    const int32_t st =
+        pair_solve<M, HAS_ED, GradAcc<Chain<M>::NE>>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, G);
+    refine_update<M>(G, right, st, live, kT, eta, T + (live ? b : 0) * M, Tout + (live ? b : 0) * M,
+                     cost ? cost + (live ? b : 0) : nullptr);
+    if (live && !right && status) status[b] = st;
+}
+
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_ragged(int32_t n, const int32_t* __restrict__ perm,
+                                                                      const int32_t* __restrict__ seg_offsets,
+                                                                      const double* __restrict__ W,
+                                                                      const double* __restrict__ T,
+                                                                      const double* __restrict__ ED, double kT,
+                                                                      double eta, double* __restrict__ Tout,
+                                                                      double* __restrict__ cost,
+                                                                      int32_t* __restrict__ status) {
+    constexpr int NW = (M + 1) * 3;
+    __shared__ Stage<M> sm;
+    const int lane = threadIdx.x;
+    const int slot = lane >> 1;
+    const bool right = lane & 1;
+    const int64_t i0 = (int64_t)blockIdx.x * TPW;
+    const int nb = (int)((n - i0) < TPW ? (n - i0) : TPW);
+    const bool live = slot < nb;
+    if (lane < TPW) sm.in.bad[lane] = 0;
+    __syncthreads();
+    int32_t b = 0;
+    int64_t s0 = 0;
+    if (live) {
+        b = perm[i0 + slot];
+        s0 = seg_offsets[b];
+        const double* gW = W + (s0 + b) * 3;
+        for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
+        for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
+    }
+    __syncthreads();
+    sanitize(sm.in, lane);
+    __syncthreads();
+    const bool valid = sm.in.bad[slot] == 0;
+    const LaneView L = make_view<M>(sm.in, slot, right);
+    GradAcc<Chain<M>::NE> G;
+#pragma unroll
+    for (int e = 0; e < Chain<M>::NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+    const int32_t st = pair_solve<M, HAS_ED, GradAcc<Chain<M>::NE>>(
+        L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, G);
+    refine_update<M>(G, right, st, live, kT, eta, T + s0, Tout + s0, cost ? cost + b : nullptr);
+    if (live && !right && status) status[b] = st;
+}
+
 // Ragged batches: one launch per segment count M over the trajectories `perm`.
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
@@ -1579,6 +1737,35 @@ hipError_t ragged_M(int32_t n, const int32_t* perm, const int32_t* so, const dou
     return hipGetLastError();
 }
 
+template <int M>
+hipError_t refine_uniform_M(int32_t B, const double* W, const double* T, const double* ED, double kT, double eta,
+                            double* Tout, double* cost, int32_t* status, hipStream_t stream) {
+    const unsigned grid = (unsigned)((B + TPW - 1) / TPW);
+    if (grid == 0) return hipSuccess;
+    if (ED)
+        hipLaunchKernelGGL((k_refine_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta, Tout,
+                           cost, status);
+    else
+        hipLaunchKernelGGL((k_refine_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta,
+                           Tout, cost, status);
+    return hipGetLastError();
+}
+
+template <int M>
+hipError_t refine_ragged_M(int32_t n, const int32_t* perm, const int32_t* so, const double* W, const double* T,
+                           const double* ED, double kT, double eta, double* Tout, double* cost, int32_t* status,
+                           hipStream_t stream) {
+    const unsigned grid = (unsigned)((n + TPW - 1) / TPW);
+    if (grid == 0) return hipSuccess;
+    if (ED)
+        hipLaunchKernelGGL((k_refine_ragged<M, true>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
+                           eta, Tout, cost, status);
+    else
+        hipLaunchKernelGGL((k_refine_ragged<M, false>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
+                           eta, Tout, cost, status);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 #ifdef TGMS_ONLY_M  // compile-only experiments: instantiate a single M
@@ -1592,6 +1779,29 @@ hipError_t launch_reduced_uniform(int M, int32_t B, const double* W, const doubl
     switch (M) {
 #define X(m) \
     case m: return uniform_M<m>(B, W, T, ED, C, status, stream);
+        TGMS_CASES(X)
+#undef X
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_refine_uniform(int M, int32_t B, const double* W, const double* T, const double* ED, double kT,
+                                 double eta, double* Tout, double* cost, int32_t* status, hipStream_t stream) {
+    switch (M) {
+#define X(m) \
+    case m: return refine_uniform_M<m>(B, W, T, ED, kT, eta, Tout, cost, status, stream);
+        TGMS_CASES(X)
+#undef X
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_refine_ragged_group(int M, int32_t n, const int32_t* perm, const int32_t* so, const double* W,
+                                      const double* T, const double* ED, double kT, double eta, double* Tout,
+                                      double* cost, int32_t* status, hipStream_t stream) {
+    switch (M) {
+#define X(m) \
+    case m: return refine_ragged_M<m>(n, perm, so, W, T, ED, kT, eta, Tout, cost, status, stream);
         TGMS_CASES(X)
 #undef X
         default: return hipErrorInvalidValue;

@@ -99,7 +99,44 @@ class Solver:
             raise TgmsError(st, self.last_error())
         return offs, out
 
+    def refine(self, seg_offsets, waypoints, seg_times, end_derivs=None, k_T: float = 1.0, eta: float = 0.1,
+               iters: int = 10, coeffs: bool = True):
+        """Time-allocation refinement on the GPU (include/tgms.h tgms_refine_batch).
+        Returns (T [S], coeffs [S,3,8] or None, cost [B], status [B], worst)."""
+        so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+        W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
+        T = np.array(seg_times, dtype=np.float64).reshape(-1)
+        ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
+        B = so.shape[0] - 1
+        C = np.zeros((int(so[-1]), 3, 8), dtype=np.float64) if coeffs else None
+        cost = np.zeros(max(B, 1), dtype=np.float64)
+        st = np.zeros(max(B, 1), dtype=np.int32)
+        worst = self._L.tgms_refine_batch(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), float(k_T), float(eta),
+                                          int(iters), _ptr(C), _ptr(cost), _ptr(st))
+        if worst in (_lib.ERR_DEVICE, _lib.ERR_NO_DEVICE):
+            raise TgmsError(worst, self.last_error())
+        return T, C, cost[:B], st[:B], worst
+
     # -------------------------------------------------------------- device API
+    def refine_uniform_device(self, B: int, M: int, d_waypoints, d_seg_times, d_seg_times_out, k_T: float,
+                              eta: float, d_cost=None, d_status=None, d_end_derivs=None, stream: int = 0) -> None:
+        st = self._L.tgms_refine_uniform_device(self._h, int(B), int(M), _ptr(d_waypoints), _ptr(d_seg_times),
+                                                _ptr(d_end_derivs), float(k_T), float(eta), _ptr(d_seg_times_out),
+                                                _ptr(d_cost), _ptr(d_status), ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
+    def refine_batch_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, d_seg_times_out,
+                            k_T: float, eta: float, d_cost=None, d_status=None, d_end_derivs=None,
+                            stream: int = 0) -> None:
+        so = np.ascontiguousarray(h_seg_offsets, dtype=np.int32)
+        st = self._L.tgms_refine_batch_device(self._h, int(so.shape[0] - 1), _ptr(so), _ptr(d_seg_offsets),
+                                              _ptr(d_waypoints), _ptr(d_seg_times), _ptr(d_end_derivs), float(k_T),
+                                              float(eta), _ptr(d_seg_times_out), _ptr(d_cost), _ptr(d_status),
+                                              ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
     def solve_uniform_device(self, B: int, M: int, d_waypoints, d_seg_times, d_coeffs, d_status=None,
                              d_end_derivs=None, stream: int = 0) -> None:
         st = self._L.tgms_solve_uniform_device(self._h, int(B), int(M), _ptr(d_waypoints), _ptr(d_seg_times),
