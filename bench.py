@@ -93,6 +93,36 @@ def cpu_baseline(B: int, M: int, target_s: float):
                       f"(LU, partial pivoting, fp64), {threads} OpenMP thread(s), {el:.1f} s"}
 
 
+def config5_line(solver, B, dev, stream, iters=10, k_T=1.0, eta=0.1, reps=3):
+    """Config 5 per GPU: ragged batch (M ~ U{2..16}) + `iters` time-refinement steps
+    + the final solve, one tgms_refine_loop_device call (planned once)."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(B, 2, 16)
+    d_so = torch.from_numpy(so.astype(np.int32)).to(dev)
+    dW = torch.from_numpy(W.reshape(-1, 3)).to(dev)
+    T0 = torch.from_numpy(T.reshape(-1)).to(dev)
+    dT = torch.empty_like(T0)
+    dC = torch.empty((int(so[-1]), 3, 8), dtype=torch.float64, device=dev)
+    dcost = torch.empty(B, dtype=torch.float64, device=dev)
+    sp = stream.cuda_stream
+
+    def run():
+        dT.copy_(T0)
+        solver.refine_loop_device(so, d_so, dW, dT, k_T, eta, iters, dC, dcost, stream=sp)
+
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"workload": f"config5: {B} ragged trajectories/GPU, M~U{{2..16}}, {iters} refinement steps + final solve",
+            "ms_per_batch": ms, "trajectories_per_s": B / (ms * 1e-3), "segments": int(so[-1]),
+            "k_T": k_T, "eta": eta}
+
+
 def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
     """Sampler on the first n solved trajectories at 100 Hz:
     Goal-layout p/v/a/j/psi/dpsi, HBM-bound by its output."""
@@ -140,6 +170,7 @@ def main():
     ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
+    ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     args = ap.parse_args()
 
@@ -227,6 +258,10 @@ def main():
                  "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
 
+    config5 = None
+    if args.config5 and M == 10:
+        config5 = config5_line(solver, B, dev, stream)
+
     sampler = None
     if args.sample_traj > 0:
         sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
@@ -268,6 +303,7 @@ def main():
             "cpu_baseline": cpu,
             "dense_kkt": dense,
             "sampler": sampler,
+            "config5": config5,
         }
         print(json.dumps(line), flush=True)
     solver.close()

@@ -122,6 +122,13 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
                                      const int32_t* d_seg_offsets, const double* d_waypoints,
                                      const double* d_seg_times, const double* d_end_derivs, double k_T, double eta,
                                      double* d_seg_times_out, double* d_cost, int32_t* d_status, void* stream);
+/* The whole config-5 pipeline on device, planned once: `iters` steps from
+ * d_seg_times (updated in place), F at the final times into d_cost (nullable) and
+ * the final solve into d_coeffs (nullable).  Uses the handle's workspace. */
+tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
+                                    const int32_t* d_seg_offsets, const double* d_waypoints, double* d_seg_times,
+                                    const double* d_end_derivs, double k_T, double eta, int32_t iters,
+                                    double* d_coeffs, double* d_cost, int32_t* d_status, void* stream);
 /* Host convenience (blocking): `iters` steps from seg_times (updated in place),
  * then F at the final times into cost (nullable) and, if coeffs is not NULL,
  * the final solve.  Returns the worst per-trajectory status. */

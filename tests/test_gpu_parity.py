@@ -287,3 +287,23 @@ def test_refine_device_step_and_errors(solver):
     finally:
         from trajectory_generator_ros2_amd import METHOD_REDUCED
         solver.set_method(METHOD_REDUCED)
+
+
+def test_refine_loop_device_matches_host(solver):
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(300, 2, 16, seed=8)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+    Th, Ch, ch, _, worst = solver.refine(so, W, T, None, 0.5, 0.2, 7)
+    assert worst == 0
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so.astype(np.int32)), d(W), d(T.copy())
+    dC = torch.empty((int(so[-1]), 3, 8), dtype=torch.float64, device="cuda")
+    dcost = torch.empty(300, dtype=torch.float64, device="cuda")
+    dst = torch.empty(300, dtype=torch.int32, device="cuda")
+    solver.refine_loop_device(so, dso, dW, dT, 0.5, 0.2, 7, dC, dcost, dst)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dT.cpu().numpy(), Th)
+    np.testing.assert_array_equal(dC.cpu().numpy(), Ch)
+    np.testing.assert_array_equal(dcost.cpu().numpy(), ch)
+    assert int(dst.abs().sum()) == 0

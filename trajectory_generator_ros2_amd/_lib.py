@@ -24,7 +24,7 @@ EXPORTS = [
     "tgms_abi_version", "tgms_status_string", "tgms_create", "tgms_destroy", "tgms_last_error",
     "tgms_set_method", "tgms_solve_batch", "tgms_solve_uniform_device", "tgms_solve_batch_device",
     "tgms_sample_count", "tgms_sample_offsets", "tgms_sample_batch", "tgms_sample_batch_device",
-    "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_batch",
+    "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_loop_device", "tgms_refine_batch",
 ]
 
 _lib = None
@@ -83,6 +83,8 @@ def load(path: str = ""):
     L.tgms_refine_uniform_device.restype = ctypes.c_int
     L.tgms_refine_batch_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, vp, vp, vp, vp]
     L.tgms_refine_batch_device.restype = ctypes.c_int
+    L.tgms_refine_loop_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp, vp]
+    L.tgms_refine_loop_device.restype = ctypes.c_int
     L.tgms_refine_batch.argtypes = [vp, i32, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp]
     L.tgms_refine_batch.restype = ctypes.c_int
     if L.tgms_abi_version() != ABI_VERSION:

@@ -124,50 +124,79 @@ tgms_status upload_plan(tgms_handle* h, int32_t B, const int32_t* so,
     return TGMS_OK;
 }
 
-tgms_status dispatch(tgms_handle* h, int32_t B, int uniform_m, const std::vector<int32_t>& counts,
-                     const int32_t* h_so, const int32_t* d_so, const double* W, const double* T,
-                     const double* ED, double* C, int32_t* st, hipStream_t stream) {
+// Launch plan of one batch: uniform M, or the trajectories grouped by M (counting
+// sort into the device permutation).  Built once per call; a refinement loop
+// reuses it for every step.
+struct Plan {
+    int uniform_m = 0;
+    std::vector<int32_t> counts, starts;
+};
+
+tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m, Plan* p, hipStream_t stream) {
+    tgms_status s = check_offsets(h, B, h_so, max_m, &p->counts, &p->uniform_m);
+    if (s != TGMS_OK || B == 0) return s;
+    if (p->uniform_m <= 0) return upload_plan(h, B, h_so, p->counts, &p->starts, stream);
+    return TGMS_OK;
+}
+
+tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
+                     const double* T, const double* ED, double* C, int32_t* st, hipStream_t stream) {
     if (B == 0) return TGMS_OK;
-    if (h->method == TGMS_METHOD_REDUCED && uniform_m > 0) {
-        TGMS_HIP(h, tgms::launch_reduced_uniform(uniform_m, B, W, T, ED, C, st, stream));
-        return TGMS_OK;
-    }
-    if (h->method == TGMS_METHOD_DENSE_KKT && uniform_m > 0) {
-        TGMS_HIP(h, tgms::launch_dense_kkt(uniform_m, B, nullptr, nullptr, W, T, ED, C, st, stream));
-        return TGMS_OK;
-    }
-    std::vector<int32_t> starts;
-    tgms_status s = upload_plan(h, B, h_so, counts, &starts, stream);
-    if (s != TGMS_OK) return s;
-    for (size_t m = 1; m < counts.size(); ++m) {
-        if (!counts[m]) continue;
-        const int32_t* ids = h->d_perm + starts[m];
+    if (p.uniform_m > 0) {
         if (h->method == TGMS_METHOD_REDUCED)
-            TGMS_HIP(h, tgms::launch_reduced_ragged_group((int)m, counts[m], ids, d_so, W, T, ED, C, st, stream));
+            TGMS_HIP(h, tgms::launch_reduced_uniform(p.uniform_m, B, W, T, ED, C, st, stream));
         else
-            TGMS_HIP(h, tgms::launch_dense_kkt((int)m, counts[m], ids, d_so, W, T, ED, C, st, stream));
+            TGMS_HIP(h, tgms::launch_dense_kkt(p.uniform_m, B, nullptr, nullptr, W, T, ED, C, st, stream));
+        return TGMS_OK;
+    }
+    for (size_t m = 1; m < p.counts.size(); ++m) {
+        if (!p.counts[m]) continue;
+        const int32_t* ids = h->d_perm + p.starts[m];
+        if (h->method == TGMS_METHOD_REDUCED)
+            TGMS_HIP(h, tgms::launch_reduced_ragged_group((int)m, p.counts[m], ids, d_so, W, T, ED, C, st, stream));
+        else
+            TGMS_HIP(h, tgms::launch_dense_kkt((int)m, p.counts[m], ids, d_so, W, T, ED, C, st, stream));
     }
     return TGMS_OK;
 }
 
 // One refinement step over a batch (uniform or ragged), reduced method only.
-tgms_status dispatch_refine(tgms_handle* h, int32_t B, int uniform_m, const std::vector<int32_t>& counts,
-                            const int32_t* h_so, const int32_t* d_so, const double* W, const double* T,
-                            const double* ED, double kT, double eta, double* Tout, double* cost, int32_t* st,
-                            hipStream_t stream) {
+tgms_status dispatch_refine(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
+                            const double* T, const double* ED, double kT, double eta, double* Tout, double* cost,
+                            int32_t* st, hipStream_t stream) {
     if (B == 0) return TGMS_OK;
-    if (uniform_m > 0) {
-        TGMS_HIP(h, tgms::launch_refine_uniform(uniform_m, B, W, T, ED, kT, eta, Tout, cost, st, stream));
+    if (p.uniform_m > 0) {
+        TGMS_HIP(h, tgms::launch_refine_uniform(p.uniform_m, B, W, T, ED, kT, eta, Tout, cost, st, stream));
         return TGMS_OK;
     }
-    std::vector<int32_t> starts;
-    tgms_status s = upload_plan(h, B, h_so, counts, &starts, stream);
-    if (s != TGMS_OK) return s;
-    for (size_t m = 1; m < counts.size(); ++m) {
-        if (!counts[m]) continue;
-        TGMS_HIP(h, tgms::launch_refine_ragged_group((int)m, counts[m], h->d_perm + starts[m], d_so, W, T, ED, kT,
-                                                     eta, Tout, cost, st, stream));
+    for (size_t m = 1; m < p.counts.size(); ++m) {
+        if (!p.counts[m]) continue;
+        TGMS_HIP(h, tgms::launch_refine_ragged_group((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED,
+                                                     kT, eta, Tout, cost, st, stream));
     }
+    return TGMS_OK;
+}
+
+// `iters` steps ping-ponging between T[0] and T[1] (the final times end in T[*cur]),
+// the cost at the final times (a step with eta = 0 leaves them unchanged), and the
+// final solve into C when it is not NULL.
+tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
+                        double* const T[2], const double* ED, double kT, double eta, int32_t iters, double* C,
+                        double* cost, int32_t* st, hipStream_t stream, int* cur) {
+    int c = 0;
+    for (int32_t k = 0; k < iters; ++k, c ^= 1) {
+        tgms_status s = dispatch_refine(h, p, B, d_so, W, T[c], ED, kT, eta, T[c ^ 1], nullptr, st, stream);
+        if (s != TGMS_OK) return s;
+    }
+    if (cost) {
+        tgms_status s = dispatch_refine(h, p, B, d_so, W, T[c], ED, kT, 0.0, T[c ^ 1], cost, st, stream);
+        if (s != TGMS_OK) return s;
+    }
+    if (C) {
+        tgms_status s = dispatch(h, p, B, d_so, W, T[c], ED, C, st, stream);
+        if (s != TGMS_OK) return s;
+    }
+    *cur = c;
     return TGMS_OK;
 }
 
@@ -248,9 +277,7 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
                              int32_t* status) {
     if (!h) return TGMS_ERR_INVALID_ARG;
     h->last_error.clear();
-    std::vector<int32_t> counts;
-    int um = 0;
-    tgms_status s = check_offsets(h, B, so, max_m_for(h), &counts, &um);
+    tgms_status s = check_offsets(h, B, so, max_m_for(h), nullptr, nullptr);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!waypoints || !seg_times || !coeffs)
@@ -279,7 +306,10 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
     TGMS_HIP(h, hipMemcpyAsync(dT, seg_times, nT * 8, hipMemcpyHostToDevice, st));
     if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
-    s = dispatch(h, B, um, counts, so, dSo, dW, dT, dED, dC, dSt, st);
+    Plan plan;
+    s = make_plan(h, B, so, max_m_for(h), &plan, st);
+    if (s != TGMS_OK) return s;
+    s = dispatch(h, plan, B, dSo, dW, dT, dED, dC, dSt, st);
     if (s != TGMS_OK) return s;
     TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     std::vector<int32_t> hst;
@@ -327,13 +357,14 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
                                     const double* dED, double* dC, int32_t* dSt, void* stream) {
     if (!h) return TGMS_ERR_INVALID_ARG;
     h->last_error.clear();
-    std::vector<int32_t> counts;
-    int um = 0;
-    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), &counts, &um);
+    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), nullptr, nullptr);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
-    return dispatch(h, B, um, counts, h_so, d_so, dW, dT, dED, dC, dSt, static_cast<hipStream_t>(stream));
+    Plan plan;
+    s = make_plan(h, B, h_so, max_m_for(h), &plan, static_cast<hipStream_t>(stream));
+    if (s != TGMS_OK) return s;
+    return dispatch(h, plan, B, d_so, dW, dT, dED, dC, dSt, static_cast<hipStream_t>(stream));
 }
 
 tgms_status tgms_refine_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* dW, const double* dT,
@@ -358,13 +389,14 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
     h->last_error.clear();
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
-    std::vector<int32_t> counts;
-    int um = 0;
-    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, &counts, &um);
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
-    return dispatch_refine(h, B, um, counts, h_so, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
+    Plan plan;
+    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, static_cast<hipStream_t>(stream));
+    if (s != TGMS_OK) return s;
+    return dispatch_refine(h, plan, B, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
                            static_cast<hipStream_t>(stream));
 }
 
@@ -376,9 +408,7 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
     if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
-    std::vector<int32_t> counts;
-    int um = 0;
-    s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, &counts, &um);
+    s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!waypoints || !seg_times) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times");
@@ -409,19 +439,13 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     TGMS_HIP(h, hipMemcpyAsync(dT[0], seg_times, S * 8, hipMemcpyHostToDevice, st));
     if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
-    int cur = 0;
-    for (int32_t k = 0; k < iters; ++k, cur ^= 1) {
-        s = dispatch_refine(h, B, um, counts, so, dSo, dW, dT[cur], dED, k_T, eta, dT[cur ^ 1], nullptr, dSt, st);
-        if (s != TGMS_OK) return s;
-    }
-    // cost at the final times (a step with eta = 0 leaves them unchanged), then the solve
-    s = dispatch_refine(h, B, um, counts, so, dSo, dW, dT[cur], dED, k_T, 0.0, dT[cur ^ 1], dCost, dSt, st);
+    Plan plan;
+    s = make_plan(h, B, so, TGMS_MAX_SEGMENTS, &plan, st);
     if (s != TGMS_OK) return s;
-    if (coeffs) {
-        s = dispatch(h, B, um, counts, so, dSo, dW, dT[cur], dED, dC, dSt, st);
-        if (s != TGMS_OK) return s;
-        TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
-    }
+    int cur = 0;
+    s = refine_loop(h, plan, B, dSo, dW, dT, dED, k_T, eta, iters, coeffs ? dC : nullptr, dCost, dSt, st, &cur);
+    if (s != TGMS_OK) return s;
+    if (coeffs) TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     TGMS_HIP(h, hipMemcpyAsync(seg_times, dT[cur], S * 8, hipMemcpyDeviceToHost, st));
     if (cost) TGMS_HIP(h, hipMemcpyAsync(cost, dCost, (size_t)B * 8, hipMemcpyDeviceToHost, st));
     std::vector<int32_t> hst;
@@ -435,6 +459,33 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     int worst = TGMS_OK;
     for (int32_t b = 0; b < B; ++b) worst = std::max(worst, (int)stout[b]);
     return (tgms_status)worst;
+}
+
+tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_so, const int32_t* d_so,
+                                    const double* dW, double* dT, const double* dED, double k_T, double eta,
+                                    int32_t iters, double* dC, double* d_cost, int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    h->last_error.clear();
+    tgms_status s = check_refine_args(h, k_T, eta);
+    if (s != TGMS_OK) return s;
+    if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    if (s != TGMS_OK) return s;
+    if (B == 0) return TGMS_OK;
+    if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t S = (size_t)h_so[B];
+    s = ensure_ws(h, align256(S * 8));
+    if (s != TGMS_OK) return s;
+    double* T[2] = {dT, static_cast<double*>(h->d_ws)};
+    Plan plan;
+    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
+    if (s != TGMS_OK) return s;
+    int cur = 0;
+    s = refine_loop(h, plan, B, d_so, dW, T, dED, k_T, eta, iters, dC, d_cost, dSt, st, &cur);
+    if (s != TGMS_OK) return s;
+    if (cur == 1) TGMS_HIP(h, hipMemcpyAsync(dT, T[1], S * 8, hipMemcpyDeviceToDevice, st));
+    return TGMS_OK;
 }
 
 int64_t tgms_sample_count(double total_T, double dt) {

@@ -126,6 +126,17 @@ class Solver:
         if st != _lib.OK:
             raise TgmsError(st, self.last_error())
 
+    def refine_loop_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, k_T: float, eta: float,
+                           iters: int, d_coeffs=None, d_cost=None, d_status=None, d_end_derivs=None,
+                           stream: int = 0) -> None:
+        so = np.ascontiguousarray(h_seg_offsets, dtype=np.int32)
+        st = self._L.tgms_refine_loop_device(self._h, int(so.shape[0] - 1), _ptr(so), _ptr(d_seg_offsets),
+                                             _ptr(d_waypoints), _ptr(d_seg_times), _ptr(d_end_derivs), float(k_T),
+                                             float(eta), int(iters), _ptr(d_coeffs), _ptr(d_cost), _ptr(d_status),
+                                             ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
     def refine_batch_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, d_seg_times_out,
                             k_T: float, eta: float, d_cost=None, d_status=None, d_end_derivs=None,
                             stream: int = 0) -> None:
