@@ -891,8 +891,18 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
     }
 }
 
-template <int M, bool HAS_ED, class Out>
-__device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, bool valid,
+// `valid` is a bool, or a callable returning it that runs after the factorisation
+// (the uniform kernel stages the waypoints there).
+template <class V>
+__device__ __forceinline__ bool get_valid(V&& v) {
+    if constexpr (std::is_same<typename std::decay<V>::type, bool>::value)
+        return v;
+    else
+        return v();
+}
+
+template <int M, bool HAS_ED, class Out, class V>
+__device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, V&& valid_src,
                                                  const double* __restrict__ ed, const Out& O) {
     using CH = Chain<M>;
     constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS, NE = CH::NE;
@@ -901,6 +911,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     MARK(ax_factor);
     AxFactors<M> Fa;
     ax_factor<M>(Fa, L, right);
+    const bool valid = get_valid(valid_src);
     MARK(ax_axisloop);
     double fin = 0.0;
 #pragma unroll 1
@@ -1051,10 +1062,11 @@ __device__ __forceinline__ void emit_all_axes(const Out& O, const LaneView& L, b
 }
 
 // Whole solve of one group (single-buffered kernels).
-template <int M, bool HAS_ED, class Out>
-__device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, bool valid,
+template <int M, bool HAS_ED, class Out, class V>
+__device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&& valid_src,
                                               const double* __restrict__ ed, const Out& O) {
     if constexpr (M <= 2) {
+        const bool valid = get_valid(valid_src);
         double u0[3][3], uM[3][3];
         const double sg = right ? -1.0 : 1.0;
 #pragma unroll
@@ -1102,11 +1114,12 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, boo
         if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
         return TGMS_OK;
     } else if constexpr (!__is_same(Out, OutCtx)) {
-        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid, ed, O);
+        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid_src, ed, O);
     } else {
 #ifndef TGMS_JOINT_AXES
-        return pair_solve_ax<M, HAS_ED, OutCtx>(L, right, valid, ed, O);
+        return pair_solve_ax<M, HAS_ED, OutCtx>(L, right, valid_src, ed, O);
 #endif
+        const bool valid = get_valid(valid_src);
         using CH = Chain<M>;
         PairState<M> S;
         ps_init<M, HAS_ED>(S, L, right, valid, ed);
@@ -1320,70 +1333,58 @@ __device__ __forceinline__ void stage_loads(In<M>& sm, const Loads<M>& R, int32_
 
 // Stage a uniform group into the raw layout: 16-B loads (indices clamped into the
 // arrays, so no lane branches), copied lane-linearly to LDS; 1/T computed in
-// registers.  Returns (wave-uniform) whether any trajectory of the group is
-// invalid; only then are per-trajectory flags built and the bad ones sanitised
-// (all-zero waypoints, unit times), which a slow path re-reads from HBM.
+// registers.  The times are issued first and staged first, so the factorisation
+// (which needs only 1/T) runs while the waypoints are still in flight.  Only a wave
+// that sees an invalid input builds per-trajectory flags (re-reading its rows from
+// HBM) and sanitises the bad trajectories (all-zero waypoints, unit times).
 template <int M>
-__device__ __forceinline__ bool stage_raw(RawIn<M>& sm, const double* __restrict__ W, const double* __restrict__ T,
-                                          int32_t B, int64_t b0, int nb, int lane) {
-    constexpr int NW = RawIn<M>::NW;
-    constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 per lane, waypoints
-    constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 per lane, times
-    const int64_t nW = (int64_t)B * NW, nT = (int64_t)B * M;
-    const int64_t jW = b0 * NW / 2, jT = b0 * M / 2;  // first double2 of the group (b0 is even)
-    const int64_t mW = nW / 2 - 1 - jW, mT = nT / 2 - 1 - jT;
-    const int jmaxW = mW < (1 << 30) ? (int)mW : (1 << 30);  // last double2 inside the arrays
-    const int jmaxT = mT < (1 << 30) ? (int)mT : (1 << 30);
-    const double2* gW = reinterpret_cast<const double2*>(W) + jW;
-    const double2* gT = reinterpret_cast<const double2*>(T) + jT;
+struct RawLoader {
+    static constexpr int NW = RawIn<M>::NW;
+    static constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 per lane, waypoints
+    static constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 per lane, times
     double2 wv[NW2], tv[NT2];
+    double wl, tl;
+    bool oddW, oddT, anyT;
+    int nw, nt;
+
+    __device__ __forceinline__ void issue(const double* __restrict__ W, const double* __restrict__ T, int32_t B,
+                                          int64_t b0, int nb, int lane) {
+        const int64_t nW = (int64_t)B * NW, nT = (int64_t)B * M;
+        const int64_t jW = b0 * NW / 2, jT = b0 * M / 2;  // first double2 of the group (b0 is even)
+        const int64_t mW = nW / 2 - 1 - jW, mT = nT / 2 - 1 - jT;
+        const int jmaxW = mW < (1 << 30) ? (int)mW : (1 << 30);  // last double2 inside the arrays
+        const int jmaxT = mT < (1 << 30) ? (int)mT : (1 << 30);
+        const double2* gW = reinterpret_cast<const double2*>(W) + jW;
+        const double2* gT = reinterpret_cast<const double2*>(T) + jT;
 #ifndef TGMS_ABL_NOLOAD
 #pragma unroll
-    for (int i = 0; i < NW2; ++i) {
-        const int j = lane + W64 * i;
-        wv[i] = gW[j < jmaxW ? j : jmaxW];
-    }
+        for (int i = 0; i < NT2; ++i) {
+            const int j = lane + W64 * i;
+            tv[i] = gT[j < jmaxT ? j : jmaxT];
+        }
 #pragma unroll
-    for (int i = 0; i < NT2; ++i) {
-        const int j = lane + W64 * i;
-        tv[i] = gT[j < jmaxT ? j : jmaxT];
-    }
+        for (int i = 0; i < NW2; ++i) {
+            const int j = lane + W64 * i;
+            wv[i] = gW[j < jmaxW ? j : jmaxW];
+        }
 #else
 #pragma unroll
-    for (int i = 0; i < NW2; ++i) wv[i] = make_double2(lane, i);
+        for (int i = 0; i < NT2; ++i) tv[i] = make_double2(1.0 + lane, 2.0);
 #pragma unroll
-    for (int i = 0; i < NT2; ++i) tv[i] = make_double2(1.0 + lane, 2.0);
+        for (int i = 0; i < NW2; ++i) wv[i] = make_double2(lane, i);
 #endif
-    const int nw = nb * NW, nt = nb * M;  // doubles of the group's live trajectories
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < NW2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        if ((TPW * NW) % (2 * W64) == 0 || e < TPW * NW) {
-            *reinterpret_cast<double2*>(sm.W + e) = wv[i];
-            bad = bad || (e < nw && !finite(wv[i].x)) || (e + 1 < nw && !finite(wv[i].y));
-        }
+        nw = nb * NW;
+        nt = nb * M;
+        // an array of odd length: its last double is outside every clamped pair
+        oddW = (nW & 1) && (b0 + nb == B);
+        oddT = (nT & 1) && (b0 + nb == B);
+        wl = oddW ? W[nW - 1] : 0.0;
+        tl = oddT ? T[nT - 1] : 1.0;
     }
-#pragma unroll
-    for (int i = 0; i < NT2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        if ((TPW * M) % (2 * W64) == 0 || e < TPW * M) {
-            *reinterpret_cast<double2*>(sm.R + e) = make_double2(fast_rcp(tv[i].x), fast_rcp(tv[i].y));
-            bad = bad || (e < nt && !finite_pos(tv[i].x)) || (e + 1 < nt && !finite_pos(tv[i].y));
-        }
-    }
-    // an array of odd length: its last double is outside every clamped pair
-    const bool oddW = (nW & 1) && (b0 + nb == B), oddT = (nT & 1) && (b0 + nb == B);
-    if (oddW || oddT) {  // tail group only (uniform branch)
-        const double wl = W[nW - 1], tl = T[nT - 1];
-        if (lane == 0) {
-            if (oddW) sm.W[nw - 1] = wl;
-            if (oddT) sm.R[nt - 1] = fast_rcp(tl);
-        }
-        bad = bad || (oddW && !finite(wl)) || (oddT && !finite_pos(tl));
-    }
-    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-    if (any_bad) {  // rare: per-trajectory flags from HBM, then sanitise
+
+    // Per-trajectory validity from HBM (rare path), sanitising the bad ones' times.
+    __device__ __forceinline__ void flags(RawIn<M>& sm, const double* __restrict__ W,
+                                          const double* __restrict__ T, int64_t b0, int nb, int lane) {
         if (lane < TPW) {
             int f = 0;
             if (lane < nb) {
@@ -1393,14 +1394,65 @@ __device__ __forceinline__ bool stage_raw(RawIn<M>& sm, const double* __restrict
                 for (int q = 0; q < M; ++q) f |= !finite_pos(t[q]);
             }
             sm.bad[lane] = f;
-            if (f) {
-                for (int q = 0; q < NW; ++q) sm.W[lane * NW + q] = 0.0;
+            if (f)
                 for (int q = 0; q < M; ++q) sm.R[lane * M + q] = 1.0;
-            }
         }
     }
-    wave_lds_sync();
-    return any_bad;
+
+    __device__ __forceinline__ void stage_T(RawIn<M>& sm, const double* __restrict__ W,
+                                            const double* __restrict__ T, int64_t b0, int nb, int lane) {
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < NT2; ++i) {
+            const int e = 2 * (lane + W64 * i);
+            if ((TPW * M) % (2 * W64) == 0 || e < TPW * M) {
+                *reinterpret_cast<double2*>(sm.R + e) = make_double2(fast_rcp(tv[i].x), fast_rcp(tv[i].y));
+                bad = bad || (e < nt && !finite_pos(tv[i].x)) || (e + 1 < nt && !finite_pos(tv[i].y));
+            }
+        }
+        if (oddT) {
+            if (lane == 0) sm.R[nt - 1] = fast_rcp(tl);
+            bad = bad || !finite_pos(tl);
+        }
+        anyT = __builtin_amdgcn_ballot_w64(bad) != 0;
+        if (anyT) flags(sm, W, T, b0, nb, lane);
+        wave_lds_sync();
+    }
+
+    // Returns (wave-uniform) whether any trajectory of the group is invalid.
+    __device__ __forceinline__ bool stage_W(RawIn<M>& sm, const double* __restrict__ W,
+                                            const double* __restrict__ T, int64_t b0, int nb, int lane) {
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < NW2; ++i) {
+            const int e = 2 * (lane + W64 * i);
+            if ((TPW * NW) % (2 * W64) == 0 || e < TPW * NW) {
+                *reinterpret_cast<double2*>(sm.W + e) = wv[i];
+                bad = bad || (e < nw && !finite(wv[i].x)) || (e + 1 < nw && !finite(wv[i].y));
+            }
+        }
+        if (oddW) {
+            if (lane == 0) sm.W[nw - 1] = wl;
+            bad = bad || !finite(wl);
+        }
+        const bool anyW = __builtin_amdgcn_ballot_w64(bad) != 0;
+        if (anyW && !anyT) flags(sm, W, T, b0, nb, lane);
+        if (anyW || anyT) {
+            if (lane < TPW && sm.bad[lane])
+                for (int q = 0; q < NW; ++q) sm.W[lane * NW + q] = 0.0;
+        }
+        wave_lds_sync();
+        return anyW || anyT;
+    }
+};
+
+template <int M>
+__device__ __forceinline__ bool stage_raw(RawIn<M>& sm, const double* __restrict__ W, const double* __restrict__ T,
+                                          int32_t B, int64_t b0, int nb, int lane) {
+    RawLoader<M> ld;
+    ld.issue(W, T, B, b0, nb, lane);
+    ld.stage_T(sm, W, T, b0, nb, lane);
+    return ld.stage_W(sm, W, T, b0, nb, lane);
 }
 
 template <int M, bool HAS_ED>
@@ -1415,7 +1467,9 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
     const int lane = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * TPW;
     const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
-    const bool any_bad = stage_raw<M>(sm.in, W, T, B, b0, nb, lane);
+    RawLoader<M> ld;
+    ld.issue(W, T, B, b0, nb, lane);
+    ld.stage_T(sm.in, W, T, b0, nb, lane);
     STAMP(1);
     // Every lane runs to the end (the output stage needs the whole wave); pairs
     // beyond nb compute on stale LDS and store nothing (their buffer range is empty).
@@ -1423,10 +1477,14 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
     const bool right = lane & 1;
     const bool live = slot < nb;
     const int64_t b = b0 + slot;
-    const bool valid = !any_bad || sm.in.bad[slot] == 0;
+    // the waypoints are staged after the factorisation (which only needs 1/T)
+    auto stage_w = [&]() {
+        const bool any_bad = ld.stage_W(sm.in, W, T, b0, nb, lane);
+        return !any_bad || sm.in.bad[slot] == 0;
+    };
     const LaneView L = make_view_raw<M>(sm.in, slot, right);
     const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane);
-    const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
     STAMP(5);
     STAMP_RT(7);
     if (live && !right && status) status[b] = st;
