@@ -914,6 +914,149 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     const bool valid = get_valid(valid_src);
     MARK(ax_axisloop);
     double fin = 0.0;
+#ifdef TGMS_AX_PIPE  // experiment (measured ~2% slower: register pressure, no ILP gain)
+    // ---- software-pipelined axes: the back substitution + emission of axis a runs
+    // step by step beside the forward substitution of axis a+1 (independent chains;
+    // the live knot set stays ~NS+1 since one array drains as the other fills) ----
+    auto start_derivs = [&](int a, double (&u0)[3]) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
+            const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
+            u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
+        }
+    };
+    auto fwd_step = [&](int a, const double (&u0)[3], double (&Y)[NS + 1][3], double (&pp)[8], int s) {
+        const int k = s + 1;
+        double pn[8];
+        rpowers(L.r(k), pn);
+        double y[3];
+        knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
+        if (s >= 1) {
+            double B[3][3], v0, v1, v2;
+            coupling(pp, B);
+            ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) Y[s][d] = y[d];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+    };
+    auto iface = [&](double (&Y)[NS + 1][3], double (&xm)[3]) {
+        double yL[3], yR[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double yv = (nR > nL) ? (right ? Y[NS - 1][d] : Y[nL - 1][d]) : Y[nL - 1][d];
+            const double yp = (d == 1) ? yv : sg * yv;
+            yL[d] = pair_even(yp);
+            yR[d] = pair_odd(yp);
+        }
+        double Cc[3][3];
+        {
+            double pc[8];
+            rpowers(L.r(nl), pc);
+            coupling(pc, Cc);
+        }
+        double g0, g1, g2;
+        ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
+        double xc0, xc1, xc2, x10, x11, x12;
+        ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
+        const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
+        const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
+        const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
+        ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
+        xm[0] = right ? -x10 : xc0;
+        xm[1] = right ? x11 : xc1;
+        xm[2] = right ? -x12 : xc2;
+        const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
+        if (nR > nL) {
+            Y[nL][0] = right ? Y[nL][0] : o0;
+            Y[nL][1] = right ? Y[nL][1] : o1;
+            Y[nL][2] = right ? Y[nL][2] : o2;
+            Y[nR][0] = right ? o0 : Y[nR][0];
+            Y[nR][1] = right ? o1 : Y[nR][1];
+            Y[nR][2] = right ? o2 : Y[nR][2];
+        } else {
+            Y[nL][0] = o0;
+            Y[nL][1] = o1;
+            Y[nL][2] = o2;
+        }
+        fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
+    };
+    auto back_step = [&](int a, double (&Y)[NS + 1][3], const double (&xm)[3], int s) {
+        const bool at_end = (s == nl - 1);
+        const bool inside = (s < nl - 1);
+        if (s + 1 < NS) {
+            double B[3][3];
+            {
+                double pb[8];
+                rpowers(L.r(s + 1), pb);
+                coupling(pb, B);
+            }
+            double b[3], x0, x1, x2;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) b[d] = Y[s][d] - (B[d][0] * Y[s + 1][0] + B[d][1] * Y[s + 1][1] + B[d][2] * Y[s + 1][2]);
+            ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
+            Y[s][0] = at_end ? xm[0] : (inside ? x0 : Y[s][0]);
+            Y[s][1] = at_end ? xm[1] : (inside ? x1 : Y[s][1]);
+            Y[s][2] = at_end ? xm[2] : (inside ? x2 : Y[s][2]);
+            fin += inside ? (x0 + x1) + x2 : 0.0;
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
+        }
+        if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR);
+    };
+    double YA[NS + 1][3], YB[NS + 1][3], xA[3], xB[3], uA[3], uB[3], pA[8], pB[8];
+    // axis 0: forward + interface
+    start_derivs(0, uA);
+    rpowers(L.r(0), pA);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        SCHED_FENCE();
+        fwd_step(0, uA, YA, pA, s);
+    }
+    SCHED_FENCE();
+    iface(YA, xA);
+    // axis 0 back/emit  ||  axis 1 forward
+    start_derivs(1, uB);
+    rpowers(L.r(0), pB);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        SCHED_FENCE();
+        back_step(0, YA, xA, NS - 1 - k);
+        fwd_step(1, uB, YB, pB, k);
+    }
+    SCHED_FENCE();
+    emit_axis<M, Out>(O, L, right, 0, 0, uA, YA[0], 0 < nR);
+    SCHED_FENCE();
+    iface(YB, xB);
+    // axis 1 back/emit  ||  axis 2 forward
+    start_derivs(2, uA);
+    rpowers(L.r(0), pA);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        SCHED_FENCE();
+        back_step(1, YB, xB, NS - 1 - k);
+        fwd_step(2, uA, YA, pA, k);
+    }
+    SCHED_FENCE();
+    emit_axis<M, Out>(O, L, right, 0, 1, uB, YB[0], 0 < nR);
+    SCHED_FENCE();
+    iface(YA, xA);
+    // axis 2 back/emit
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        SCHED_FENCE();
+        back_step(2, YA, xA, NS - 1 - k);
+    }
+    SCHED_FENCE();
+    emit_axis<M, Out>(O, L, right, 0, 2, uA, YA[0], 0 < nR);
+#else
 #pragma unroll 1
     for (int a = 0; a < 3; ++a) {
         // virtual-frame start derivatives of this axis: even lane u0, odd lane P uM
@@ -1002,7 +1145,9 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             }
             fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
         }
-        // ---- back substitution ----
+        // ---- back substitution, each segment emitted as soon as its end knots are
+        // final (segment s+1 right after knot s): the two are independent, which
+        // gives the scheduler a second dependency chain to interleave ----
         MARK(ax_back);
 #pragma unroll
         for (int s = NS - 1; s >= 0; --s) {
@@ -1028,9 +1173,15 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #pragma unroll
                 for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
             }
+#ifndef TGMS_AX_EMIT_AFTER
+            if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR);
+#endif
         }
-        // ---- emission of this axis ----
         MARK(ax_emit);
+#ifndef TGMS_AX_EMIT_AFTER
+        SCHED_FENCE();
+        emit_axis<M, Out>(O, L, right, 0, a, u0, Y[0], 0 < nR);
+#else
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             SCHED_FENCE();
@@ -1039,7 +1190,9 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             for (int d = 0; d < 3; ++d) xs[d] = (e == 0) ? u0[d] : Y[e >= 1 ? e - 1 : 0][d];
             emit_axis<M, Out>(O, L, right, e, a, xs, Y[e], e < nR);
         }
+#endif
     }
+#endif
     MARK(ax_end);
     const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
