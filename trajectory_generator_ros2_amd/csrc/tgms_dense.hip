@@ -1,10 +1,20 @@
 // tgms_dense.hip — TGMS_METHOD_DENSE_KKT: the survey's literal a1-a3 on gfx950.
 //
-// One WAVEFRONT per trajectory; [[2Q, A^T],[A, 0]] (snap
-// Hessian Q, a2: endpoint/continuity rows A with right-hand side b) is assembled
-// in LDS (N = 14M+2, N^2*8 B = 161,312 B at M = 10); LU with partial pivoting,
-// lanes over rows for the pivot search / multipliers and over columns for the
-// rank-1 update; the 3 right-hand sides live in registers of the row-owner lanes.
+// One WORKGROUP (NWV = 16 wavefronts) per trajectory; [[2Q, A^T],[A, 0]] (SURVEY.md
+// §8(a) a1: snap Hessian Q, a2: endpoint/continuity rows A with right-hand side b) is
+// assembled in LDS (N = 14M+2, N^2*8 B = 161,312 B at M = 10, so one trajectory per CU
+// and all its parallelism is inside the workgroup).  LU with partial pivoting:
+//   - rows never move; a position -> row permutation lives in registers (identical in
+//     every wave), so a step has exactly one workgroup barrier;
+//   - the rank-1 update of step k deals rows round-robin to the waves (lanes over
+//     columns, rows with a zero multiplier skipped: the KKT stays sparse for a long
+//     time); while updating, each wave also finds its best pivot candidate for column
+//     k+1 and leaves it in a double-buffered LDS slot, so the pivot search of step k+1
+//     is NWV LDS reads, not a column scan and shuffle reduction;
+//   - the 3 right-hand sides live in wave 0's registers (lane = position), eliminated
+//     on the fly; wave 0 back-substitutes with the stored inverse pivots.
+// Measured (M = 10, B = 65536): 228 ms with one wave per trajectory -> ~122 ms; the
+// per-step phase profile (scripts/dstamps.py) is LDS-latency bound, see DESIGN.md.
 #include "tgms_device.h"
 #include "tgms_internal.h"
 
@@ -24,25 +34,53 @@ __device__ __forceinline__ double ipow(double t, int e) {
     return p;
 }
 
-__device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, W64); }
+// broadcast lane src (wave-uniform) to the wave: two v_readlane, no LDS round trip
+__device__ __forceinline__ double bcast(double v, int src) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, src);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), src);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+#ifndef TGMS_DENSE_NWV
+#define TGMS_DENSE_NWV 16
+#endif
+constexpr int NWV = TGMS_DENSE_NWV;
+#ifdef TGMS_DENSE_STAMPS  // diagnostic build: per-step phase timestamps of wave 0 in blocks < 64
+constexpr int DST_BLOCKS = 64, DST_STEPS = 160;
+__device__ unsigned long long g_dstamps[DST_BLOCKS * DST_STEPS * 4];
+#define DSTAMP(k, i)                                                                          \
+    do {                                                                                      \
+        asm volatile("" ::: "memory");                                                        \
+        if (bi < DST_BLOCKS && tid == 0)                                                      \
+            g_dstamps[(bi * DST_STEPS + (k)) * 4 + (i)] = __builtin_amdgcn_s_memtime();       \
+    } while (0)
+#else
+#define DSTAMP(k, i) \
+    do {             \
+    } while (0)
+#endif
+#ifndef TGMS_DENSE_DR
+#define TGMS_DENSE_DR 1
+#endif
+constexpr int DR = TGMS_DENSE_DR;  // rows per rank-1 update batch
 
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64) void k_dense_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
-                                                  const int32_t* __restrict__ seg_offsets,
-                                                  const double* __restrict__ W,
-                                                  const double* __restrict__ T,
-                                                  const double* __restrict__ ED,
-                                                  double* __restrict__ C,
-                                                  int32_t* __restrict__ status) {
+__global__ __launch_bounds__(W64 * NWV) void k_dense_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
+                                                          const int32_t* __restrict__ seg_offsets,
+                                                          const double* __restrict__ W,
+                                                          const double* __restrict__ T,
+                                                          const double* __restrict__ ED,
+                                                          double* __restrict__ C,
+                                                          int32_t* __restrict__ status) {
     constexpr int n = 8 * M;
     constexpr int m = 8 + 6 * (M - 1);
     constexpr int N = n + m;
     constexpr int S = (N + W64 - 1) / W64;  // rows (and columns) per lane
     extern __shared__ double smem[];
-    double* A = smem;          // N x N row-major KKT
-    double* lcol = smem + N * N;  // multipliers of the current column
+    double* A = smem;             // N x N row-major KKT
 
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar loop bounds
     const int32_t bi = blockIdx.x;
     if (bi >= n_traj) return;
     const int32_t b = ids ? ids[bi] : bi;
@@ -54,23 +92,24 @@ __global__ __launch_bounds__(64) void k_dense_kkt(int32_t n_traj, const int32_t*
     bool valid = true;
     for (int i = 0; i < M; ++i) valid = valid && finite_pos(tt[i]);
     {
-        double s = 0.0;
-        for (int q = 0; q < (M + 1) * 3; ++q) s += w[q] * 0.0;
+        double sum = 0.0;
+        for (int q = 0; q < (M + 1) * 3; ++q) sum += w[q] * 0.0;
         if (HAS_ED)
-            for (int q = 0; q < 18; ++q) s += ed[q] * 0.0;
-        valid = valid && (s == 0.0);
+            for (int q = 0; q < 18; ++q) sum += ed[q] * 0.0;
+        valid = valid && (sum == 0.0);
     }
 
-    for (int e = lane; e < N * N; e += W64) A[e] = 0.0;
+    DSTAMP(N + 1, 0);
+    for (int e = tid; e < N * N; e += W64 * NWV) A[e] = 0.0;
     __syncthreads();
     // a1: 2Q blocks
-    for (int e = lane; e < M * 16; e += W64) {
+    for (int e = tid; e < M * 16; e += W64 * NWV) {
         const int i = e >> 4, j = 4 + ((e >> 2) & 3), k = 4 + (e & 3);
         const int ex = j + k - 7;
         A[(8 * i + j) * N + 8 * i + k] = 2.0 * dfac(j, 4) * dfac(k, 4) * ipow(tt[i], ex) / (double)ex;
     }
-    // a2: constraint rows (and their transposes), one lane per row
-    for (int r = lane; r < m; r += W64) {
+    // a2: constraint rows (and their transposes), one thread per row
+    for (int r = tid; r < m; r += W64 * NWV) {
         double* rowp = A + (n + r) * N;
         auto put = [&](int col, double v) {
             rowp[col] = v;
@@ -96,7 +135,7 @@ __global__ __launch_bounds__(64) void k_dense_kkt(int32_t n_traj, const int32_t*
             }
         }
     }
-    // right-hand sides in registers: lane owns rows lane + 64*s
+    // right-hand sides in wave 0's registers: lane owns rows lane + 64*s
     double rhs[S][3];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -118,94 +157,205 @@ __global__ __launch_bounds__(64) void k_dense_kkt(int32_t n_traj, const int32_t*
     }
     __syncthreads();
 
-    // a3: LU with partial pivoting
+    // a3: LU with partial pivoting.  Rows never move: permv (registers; every wave holds
+    // the same copy) maps elimination position -> physical row, so a step needs one
+    // barrier: each wave repeats the pivot search on column k, then updates the rows it
+    // owns (positions k+1+wave, k+1+wave+NWV, ...); wave 0 also the right-hand sides.
+    static_assert(S <= 3, "N <= 192");
+    int permv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) permv[s] = lane + W64 * s;
+    auto perm_at = [&](int pos) -> int {  // wave-uniform position -> physical row
+        // read every slot, select the scalar (a select on permv itself is folded into
+        // an indexed access, i.e. scratch)
+        const int l = pos & 63;
+        int v = __builtin_amdgcn_readlane(permv[0], l);
+        if constexpr (S > 1) v = pos >= W64 ? __builtin_amdgcn_readlane(permv[1], l) : v;
+        if constexpr (S > 2) v = pos >= 2 * W64 ? __builtin_amdgcn_readlane(permv[S - 1], l) : v;
+        return v;
+    };
+    // per-wave pivot candidates for column k+1, found while updating step k's rows
+    // (double-buffered by step parity: a step's readers finish before the next writers)
+    __shared__ double cand_v[2][NWV];
+    __shared__ int cand_i[2][NWV];
+    __shared__ double ipiv_s[N];  // 1 / pivot of each position, for the back substitution
     bool singular = false;
     for (int k = 0; k < N; ++k) {
+        const int ks = k / W64, kl = k % W64;
+        DSTAMP(k, 0);
         double best = -1.0;
         int bidx = N;
+        if (k == 0) {  // first column: a full search (later columns: candidates of step k-1)
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int i = lane + W64 * s;
-            if (i >= k && i < N) {
-                const double v = fabs(A[i * N + k]);
-                if (v > best) { best = v; bidx = i; }
+            for (int s = 0; s < S; ++s) {
+                const int i = lane + W64 * s;
+                if (i < N) {
+                    const double v = fabs(A[permv[s] * N]);
+                    if (v > best) {
+                        best = v;
+                        bidx = i;
+                    }
+                }
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const double ov = __shfl_xor(best, off, W64);
+                const int oi = __shfl_xor(bidx, off, W64);
+                if (ov > best || (ov == best && oi < bidx)) {
+                    best = ov;
+                    bidx = oi;
+                }
+            }
+        } else {  // max |.|, ties to the lowest position: the same order as the full search
+            const double* cb = cand_v[(k - 1) & 1];
+            const int* ci = cand_i[(k - 1) & 1];
+            double ov[NWV];
+            int oi[NWV];
+#pragma unroll
+            for (int q = 0; q < NWV; ++q) {  // all loads in flight, then branch-free selects
+                ov[q] = cb[q];
+                oi[q] = ci[q];
+            }
+#pragma unroll
+            for (int q = 0; q < NWV; ++q) {
+                const bool take = (ov[q] > best) | ((ov[q] == best) & (oi[q] < bidx));
+                best = take ? ov[q] : best;
+                bidx = take ? oi[q] : bidx;
             }
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double ov = __shfl_xor(best, off, W64);
-            const int oi = __shfl_xor(bidx, off, W64);
-            if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+#ifdef TGMS_DENSE_ABL_NOPIV  // ablation (timing only): no pivot search
+        best = 1.0;
+        bidx = k;
+#endif
+#ifdef TGMS_DENSE_ABL_NOSING  // ablation (timing only): never stop early
+        if (false) {
+#else
+        if (!__builtin_amdgcn_readfirstlane(best > 0.0)) {  // identical in every wave
+#endif
+            singular = true;
+            break;
         }
-        if (!(best > 0.0)) { singular = true; break; }
-        const int p = bidx;
-        const int ks = k / W64, kl = k % W64, ps = p / W64, pl = p % W64;
+        const int p = __builtin_amdgcn_readfirstlane(bidx);
         if (p != k) {
-            for (int j = k + lane; j < N; j += W64) {
-                const double t = A[k * N + j];
-                A[k * N + j] = A[p * N + j];
-                A[p * N + j] = t;
+            const int ps = p / W64, pl = p % W64;
+            const int rk = perm_at(k), rp = perm_at(p);
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int i = lane + W64 * s;
+                permv[s] = i == k ? rp : (i == p ? rk : permv[s]);
             }
+            if (wave == 0) {
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double vk = 0.0, vp = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    double vk = 0.0, vp = 0.0;
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (s == ks) vk = rhs[s][a];
-                    if (s == ps) vp = rhs[s][a];
+                    for (int s = 0; s < S; ++s) {
+                        if (s == ks) vk = rhs[s][a];
+                        if (s == ps) vp = rhs[s][a];
+                    }
+                    vk = bcast(vk, kl);
+                    vp = bcast(vp, pl);
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if (s == ks && lane == kl) rhs[s][a] = vp;
+                        if (s == ps && lane == pl) rhs[s][a] = vk;
+                    }
                 }
-                vk = bcast(vk, kl);
-                vp = bcast(vp, pl);
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if (s == ks && lane == kl) rhs[s][a] = vp;
-                    if (s == ps && lane == pl) rhs[s][a] = vk;
-                }
             }
         }
-        __syncthreads();
-        const double ipiv = 1.0 / A[k * N + k];
-        double rk[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            double v = 0.0;
-#pragma unroll
-            for (int s = 0; s < S; ++s)
-                if (s == ks) v = rhs[s][a];
-            rk[a] = bcast(v, kl);
-        }
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int i = lane + W64 * s;
-            if (i > k && i < N) {
-                const double l = A[i * N + k] * ipiv;
-                lcol[i] = l;
-#pragma unroll
-                for (int a = 0; a < 3; ++a) rhs[s][a] -= l * rk[a];
-            }
-        }
-        __syncthreads();
+        DSTAMP(k, 1);
+        const double* uk = A + perm_at(k) * N;
+        const double ipiv = 1.0 / uk[k];
+        if (tid == 0) ipiv_s[k] = ipiv;
         double u[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int j = k + 1 + lane + W64 * s;
-            u[s] = (j < N) ? A[k * N + j] : 0.0;
+            u[s] = (j < N) ? uk[j] : 0.0;
         }
-        for (int i = k + 1; i < N; ++i) {
-            const double l = lcol[i];
-            if (l == 0.0) continue;  // wave-uniform: the KKT stays sparse for many steps
-            double* rowi = A + i * N + k + 1 + lane;
+        if (wave == 0) {
+            double rk[3];
 #pragma unroll
-            for (int s = 0; s < S; ++s)
-                if (k + 1 + lane + W64 * s < N) rowi[W64 * s] -= l * u[s];
+            for (int a = 0; a < 3; ++a) {
+                double v = 0.0;
+#pragma unroll
+                for (int s = 0; s < S; ++s)
+                    if (s == ks) v = rhs[s][a];
+                rk[a] = bcast(v, kl);
+            }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int i = lane + W64 * s;
+                if (i > k && i < N) {
+                    const double l = A[permv[s] * N + k] * ipiv;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) rhs[s][a] -= l * rk[a];
+                }
+            }
         }
+        DSTAMP(k, 2);
+        const double u1 = (k + 1 < N) ? uk[k + 1] : 0.0;  // = u[0] in lane 0
+        double cbest = -1.0;
+        int cidx = N;
+        // rank-1 update, DR rows per batch so their LDS reads overlap; rows whose
+        // multiplier is zero (most of them early on: the KKT is sparse) are skipped
+#ifdef TGMS_DENSE_ABL_NOUPD  // ablation (timing only): no rank-1 update
+        for (int pos0 = N; pos0 < N; pos0 += NWV * DR) {
+#else
+        for (int pos0 = k + 1 + wave; pos0 < N; pos0 += NWV * DR) {
+#endif
+            int ph[DR];
+            double l[DR], a1[DR];
+#pragma unroll
+            for (int r = 0; r < DR; ++r) {
+                const int pos = pos0 + NWV * r;  // loads unconditional (clamped): one wait
+                ph[r] = perm_at(pos < N ? pos : N - 1);
+                const double akr = A[ph[r] * N + k];
+                a1[r] = (k + 1 < N) ? A[ph[r] * N + k + 1] : 0.0;
+                l[r] = pos < N ? akr * ipiv : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < DR; ++r) {  // this row's column k+1 after the update
+                const int pos = pos0 + NWV * r;
+                const double c = fabs(l[r] != 0.0 ? __builtin_fma(-l[r], u1, a1[r]) : a1[r]);
+                const bool take = (pos < N) & (c > cbest);
+                cbest = take ? c : cbest;
+                cidx = take ? pos : cidx;
+            }
+            double v[DR][S];
+#pragma unroll
+            for (int r = 0; r < DR; ++r)
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int j = k + 1 + lane + W64 * s;
+                    v[r][s] = (l[r] != 0.0 && j < N) ? A[ph[r] * N + j] : 0.0;
+                }
+#pragma unroll
+            for (int r = 0; r < DR; ++r)
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int j = k + 1 + lane + W64 * s;
+                    if (l[r] != 0.0 && j < N) A[ph[r] * N + j] = __builtin_fma(-l[r], u[s], v[r][s]);
+                }
+        }
+        if (lane == 0) {
+            cand_v[k & 1][wave] = cbest;
+            cand_i[k & 1][wave] = cidx;
+        }
+        DSTAMP(k, 3);
         __syncthreads();
     }
-    // back substitution (column oriented); x overwrites rhs
+    DSTAMP(N, 0);
+    if (wave != 0) return;
+    // back substitution (column oriented, wave 0); x overwrites rhs
+#ifdef TGMS_DENSE_ABL_NOBS  // ablation (timing only)
+    if (false) {
+#else
     if (!singular) {
+#endif
         for (int k = N - 1; k >= 0; --k) {
             const int ks = k / W64, kl = k % W64;
-            const double ipiv = 1.0 / A[k * N + k];
+            const double ipiv = ipiv_s[k];
             double xk[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -222,13 +372,14 @@ __global__ __launch_bounds__(64) void k_dense_kkt(int32_t n_traj, const int32_t*
 #pragma unroll
                     for (int a = 0; a < 3; ++a) rhs[s][a] = xk[a];
                 } else if (i < k) {
-                    const double aik = A[i * N + k];
+                    const double aik = A[permv[s] * N + k];
 #pragma unroll
                     for (int a = 0; a < 3; ++a) rhs[s][a] -= aik * xk[a];
                 }
             }
         }
     }
+    DSTAMP(N, 1);
     // a4: coefficients [seg][axis][8]
     double fin = 0.0;
     double* out = C + s0 * 24;
@@ -262,19 +413,19 @@ hipError_t dense_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const 
                    const double* T, const double* ED, double* C, int32_t* status,
                    hipStream_t stream) {
     constexpr int N = 14 * M + 2;
-    const size_t lds = sizeof(double) * (size_t)(N * N + N);
+    const size_t lds = sizeof(double) * (size_t)(N * N);
     if (n_traj <= 0) return hipSuccess;
     hipError_t e;
     if (ED) {
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dense_kkt<M, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dense_kkt<M, true>), dim3(n_traj), dim3(W64), lds, stream, n_traj, ids, so, W, T, ED, C, status);
+        hipLaunchKernelGGL((k_dense_kkt<M, true>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
     } else {
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dense_kkt<M, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dense_kkt<M, false>), dim3(n_traj), dim3(W64), lds, stream, n_traj, ids, so, W, T, ED, C, status);
+        hipLaunchKernelGGL((k_dense_kkt<M, false>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
     }
     return hipGetLastError();
 }
@@ -294,3 +445,9 @@ hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* ids, const int
 }
 
 }  // namespace tgms
+
+#ifdef TGMS_DENSE_STAMPS
+extern "C" int tgms_debug_dense_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tgms::g_dstamps), sizeof(unsigned long long) * (size_t)n) == hipSuccess;
+}
+#endif
