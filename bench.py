@@ -123,6 +123,27 @@ def config5_line(solver, B, dev, stream, iters=10, k_T=1.0, eta=0.1, reps=3):
             "k_T": k_T, "eta": eta}
 
 
+def host_line(solver, B, M, W, T, reps=3):
+    """PCIe-inclusive rate: tgms_solve_batch on host buffers (H2D, solve, D2H), the call
+    the node makes; reported beside `value`, never as it (SURVEY.md 8(d) timing)."""
+    import numpy as np
+    so = (np.arange(B + 1, dtype=np.int32) * M)
+    Wf, Tf = W.reshape(-1, 3), T.reshape(-1)
+    out = (np.zeros((B * M, 3, 8)), np.zeros(B, dtype=np.int32))  # caller-owned, reused
+    C, st, worst = solver.solve(so, Wf, Tf, out=out)  # warm-up (workspace, page faults)
+    assert worst == 0, worst
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        C, st, worst = solver.solve(so, Wf, Tf, out=out)
+        ts.append(time.perf_counter() - t0)
+    ms = sorted(ts)[len(ts) // 2] * 1e3
+    nbytes = algorithmic_bytes_per_traj(M) * B + (B + 1) * 4
+    return {"trajectories": B, "ms_per_call": ms, "trajectories_per_s": B / (ms * 1e-3),
+            "pcie_bytes": nbytes, "effective_GBs": nbytes / (ms * 1e-3) / 1e9,
+            "path": "tgms_solve_batch, pageable host numpy buffers reused across calls"}
+
+
 def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
     """Sampler on the first n solved trajectories at 100 Hz:
     Goal-layout p/v/a/j/psi/dpsi, HBM-bound by its output."""
@@ -171,6 +192,7 @@ def main():
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
     ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
+    ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     args = ap.parse_args()
 
@@ -266,6 +288,10 @@ def main():
     if args.sample_traj > 0:
         sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
 
+    host = None
+    if args.host_line and rank == 0:
+        host = host_line(solver, B, M, W, T)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(B, M, args.cpu_seconds)
@@ -304,6 +330,7 @@ def main():
             "dense_kkt": dense,
             "sampler": sampler,
             "config5": config5,
+            "host_path": host,
         }
         print(json.dumps(line), flush=True)
     solver.close()

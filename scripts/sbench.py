@@ -10,6 +10,8 @@ from trajectory_generator_ros2_amd.solver import Solver, sample_offsets
 
 N = int(os.environ.get("SB_N", 4096)); M = 10; dt = float(os.environ.get("SB_DT", 0.01))
 _, W, T = S.uniform_batch(N, M)
+if os.environ.get("SB_CONST_T"):  # equal-length trajectories: no tail imbalance
+    T[:] = float(os.environ["SB_CONST_T"])
 s = Solver(0)
 dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
 dC = torch.empty((N, M, 3, 8), dtype=torch.float64, device="cuda")

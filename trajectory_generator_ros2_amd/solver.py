@@ -67,17 +67,27 @@ class Solver:
         self.method = method
 
     # ---------------------------------------------------------------- host API
-    def solve(self, seg_offsets, waypoints, seg_times, end_derivs=None, check: bool = True
-              ) -> Tuple[np.ndarray, np.ndarray, int]:
-        """CSR host batch -> (coeffs [S,3,8], status [B], worst status)."""
+    def solve(self, seg_offsets, waypoints, seg_times, end_derivs=None, check: bool = True,
+              out: Optional[Tuple[np.ndarray, np.ndarray]] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+        """CSR host batch -> (coeffs [S,3,8], status [B], worst status).
+
+        `out` = (coeffs, status) reuses caller buffers (float64 [S,3,8], int32 [>=B]):
+        fresh host pages fault in during the device-to-host copy, reused ones do not."""
         so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
         W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
         T = np.ascontiguousarray(seg_times, dtype=np.float64).reshape(-1)
         ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
         B = so.shape[0] - 1
         S = int(so[-1]) if B > 0 else 0
-        C = np.zeros((S, 3, 8), dtype=np.float64)
-        st = np.zeros(max(B, 1), dtype=np.int32)
+        if out is not None:
+            C, st = out
+            if C.dtype != np.float64 or C.size < S * 24 or not C.flags.c_contiguous:
+                raise ValueError("out coeffs must be C-contiguous float64 with >= S*24 elements")
+            if st.dtype != np.int32 or st.size < max(B, 1) or not st.flags.c_contiguous:
+                raise ValueError("out status must be C-contiguous int32 with >= B elements")
+        else:
+            C = np.zeros((S, 3, 8), dtype=np.float64)
+            st = np.zeros(max(B, 1), dtype=np.int32)
         worst = self._L.tgms_solve_batch(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), _ptr(C), _ptr(st))
         if check and worst not in (_lib.OK,) and worst in (_lib.ERR_DEVICE, _lib.ERR_NO_DEVICE):
             raise TgmsError(worst, self.last_error())
