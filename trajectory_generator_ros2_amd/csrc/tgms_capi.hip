@@ -14,9 +14,15 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
+
+#ifndef TGMS_AUX_STREAMS
+#define TGMS_AUX_STREAMS 4
+#endif
 
 struct tgms_handle {
     int device = 0;
@@ -31,6 +37,29 @@ struct tgms_handle {
     int32_t* h_perm = nullptr;  // pinned staging of the plan
     size_t h_perm_cap = 0;
     hipEvent_t perm_ev = nullptr;  // guards h_perm reuse until the upload completed
+    // ragged plans: the per-M group launches fork onto these streams and join back, so
+    // the groups (each a few hundred wavefronts) run side by side instead of in series
+    hipStream_t aux[TGMS_AUX_STREAMS] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[TGMS_AUX_STREAMS] = {};
+    bool aux_ready = false;
+    // tgms_refine_loop_device: the whole loop (K steps x every M group) captured once
+    // into a HIP graph and replayed while its arguments and plan are unchanged
+    struct LoopKey {
+        int32_t B = -1, iters = 0;
+        const void *d_so, *dW, *dT, *dT2, *dED, *dC, *d_cost, *dSt, *d_perm;
+        double k_T, eta;
+        std::vector<int32_t> counts, starts;
+        int uniform_m;
+        bool operator==(const LoopKey& o) const {
+            return B == o.B && iters == o.iters && d_so == o.d_so && dW == o.dW && dT == o.dT && dT2 == o.dT2 &&
+                   dED == o.dED && dC == o.dC && d_cost == o.d_cost && dSt == o.dSt && d_perm == o.d_perm &&
+                   k_T == o.k_T && eta == o.eta && counts == o.counts && starts == o.starts &&
+                   uniform_m == o.uniform_m;
+        }
+    } loop_key;
+    hipGraphExec_t loop_exec = nullptr;
+    hipStream_t cap_stream = nullptr;
 };
 
 namespace {
@@ -139,6 +168,63 @@ tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m,
     return TGMS_OK;
 }
 
+tgms_status ensure_aux(tgms_handle* h) {
+    if (h->aux_ready) return TGMS_OK;
+    TGMS_HIP(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+    for (int j = 0; j < TGMS_AUX_STREAMS; ++j) {
+        TGMS_HIP(h, hipStreamCreateWithFlags(&h->aux[j], hipStreamNonBlocking));
+        TGMS_HIP(h, hipEventCreateWithFlags(&h->join_ev[j], hipEventDisableTiming));
+    }
+    h->aux_ready = true;
+    return TGMS_OK;
+}
+
+// Run independent launches (each `hipError_t(hipStream_t)`): one goes on `stream`;
+// several fork onto the auxiliary streams and join back, so `stream` order is kept
+// for the caller.
+tgms_status run_parallel(tgms_handle* h, hipStream_t stream,
+                         const std::vector<std::function<hipError_t(hipStream_t)>>& jobs) {
+    if (jobs.size() <= 1 || TGMS_AUX_STREAMS <= 1) {
+        for (auto& j : jobs) TGMS_HIP(h, j(stream));
+        return TGMS_OK;
+    }
+    tgms_status s = ensure_aux(h);
+    if (s != TGMS_OK) return s;
+    const int used = (int)std::min<size_t>(jobs.size(), TGMS_AUX_STREAMS);
+    TGMS_HIP(h, hipEventRecord(h->fork_ev, stream));
+    for (int j = 0; j < used; ++j) TGMS_HIP(h, hipStreamWaitEvent(h->aux[j], h->fork_ev, 0));
+    for (size_t g = 0; g < jobs.size(); ++g) TGMS_HIP(h, jobs[g](h->aux[g % used]));
+    for (int j = 0; j < used; ++j) {
+        TGMS_HIP(h, hipEventRecord(h->join_ev[j], h->aux[j]));
+        TGMS_HIP(h, hipStreamWaitEvent(stream, h->join_ev[j], 0));
+    }
+    return TGMS_OK;
+}
+
+// Reduced method, ragged plan: every M group in one launch per occupancy class
+// (M <= 11 / M >= 12), the longest groups' wavefronts first.
+tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, bool refine, const int32_t* d_so,
+                             const double* W, const double* T, const double* ED, double kT, double eta,
+                             double* Tout, double* cost, double* C, int32_t* st) {
+    tgms::GroupTable tab[2] = {};
+    for (size_t m = p.counts.size(); m-- > 1;) {
+        if (!p.counts[m]) continue;
+        tgms::GroupTable& t = tab[m >= 12 ? 1 : 0];
+        const int g = t.ngroups++;
+        t.m[g] = (int32_t)m;
+        t.n[g] = p.counts[m];
+        t.perm[g] = h->d_perm + p.starts[m];
+        t.blk_end[g] = (g ? t.blk_end[g - 1] : 0) + (p.counts[m] + tgms::RAGGED_TPW - 1) / tgms::RAGGED_TPW;
+    }
+    std::vector<std::function<hipError_t(hipStream_t)>> jobs;
+    for (int c = 1; c >= 0; --c)
+        if (tab[c].ngroups)
+            jobs.push_back([&, c](hipStream_t q) {
+                return tgms::launch_ragged_multi(c, tab[c], refine, d_so, W, T, ED, kT, eta, Tout, cost, C, st, q);
+            });
+    return run_parallel(h, stream, jobs);
+}
+
 tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
                      const double* T, const double* ED, double* C, int32_t* st, hipStream_t stream) {
     if (B == 0) return TGMS_OK;
@@ -149,15 +235,15 @@ tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_
             TGMS_HIP(h, tgms::launch_dense_kkt(p.uniform_m, B, nullptr, nullptr, W, T, ED, C, st, stream));
         return TGMS_OK;
     }
-    for (size_t m = 1; m < p.counts.size(); ++m) {
-        if (!p.counts[m]) continue;
-        const int32_t* ids = h->d_perm + p.starts[m];
-        if (h->method == TGMS_METHOD_REDUCED)
-            TGMS_HIP(h, tgms::launch_reduced_ragged_group((int)m, p.counts[m], ids, d_so, W, T, ED, C, st, stream));
-        else
-            TGMS_HIP(h, tgms::launch_dense_kkt((int)m, p.counts[m], ids, d_so, W, T, ED, C, st, stream));
-    }
-    return TGMS_OK;
+    if (h->method == TGMS_METHOD_REDUCED)
+        return run_ragged_multi(h, p, stream, false, d_so, W, T, ED, 0.0, 0.0, nullptr, nullptr, C, st);
+    std::vector<std::function<hipError_t(hipStream_t)>> jobs;
+    for (size_t m = p.counts.size(); m-- > 1;)
+        if (p.counts[m])
+            jobs.push_back([&, m](hipStream_t q) {
+                return tgms::launch_dense_kkt((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED, C, st, q);
+            });
+    return run_parallel(h, stream, jobs);
 }
 
 // One refinement step over a batch (uniform or ragged), reduced method only.
@@ -169,12 +255,7 @@ tgms_status dispatch_refine(tgms_handle* h, const Plan& p, int32_t B, const int3
         TGMS_HIP(h, tgms::launch_refine_uniform(p.uniform_m, B, W, T, ED, kT, eta, Tout, cost, st, stream));
         return TGMS_OK;
     }
-    for (size_t m = 1; m < p.counts.size(); ++m) {
-        if (!p.counts[m]) continue;
-        TGMS_HIP(h, tgms::launch_refine_ragged_group((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED,
-                                                     kT, eta, Tout, cost, st, stream));
-    }
-    return TGMS_OK;
+    return run_ragged_multi(h, p, stream, true, d_so, W, T, ED, kT, eta, Tout, cost, nullptr, st);
 }
 
 // `iters` steps ping-ponging between T[0] and T[1] (the final times end in T[*cur]),
@@ -258,6 +339,13 @@ void tgms_destroy(tgms_handle* h) {
     if (h->d_perm) (void)hipFree(h->d_perm);
     if (h->h_perm) (void)hipHostFree(h->h_perm);
     if (h->perm_ev) (void)hipEventDestroy(h->perm_ev);
+    for (int j = 0; j < TGMS_AUX_STREAMS; ++j) {
+        if (h->aux[j]) (void)hipStreamDestroy(h->aux[j]);
+        if (h->join_ev[j]) (void)hipEventDestroy(h->join_ev[j]);
+    }
+    if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+    if (h->loop_exec) (void)hipGraphExecDestroy(h->loop_exec);
+    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -481,10 +569,44 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     Plan plan;
     s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
     if (s != TGMS_OK) return s;
-    int cur = 0;
-    s = refine_loop(h, plan, B, d_so, dW, T, dED, k_T, eta, iters, dC, d_cost, dSt, st, &cur);
-    if (s != TGMS_OK) return s;
-    if (cur == 1) TGMS_HIP(h, hipMemcpyAsync(dT, T[1], S * 8, hipMemcpyDeviceToDevice, st));
+    auto body = [&](hipStream_t q) -> tgms_status {
+        int cur = 0;
+        tgms_status r = refine_loop(h, plan, B, d_so, dW, T, dED, k_T, eta, iters, dC, d_cost, dSt, q, &cur);
+        if (r != TGMS_OK) return r;
+        if (cur == 1) TGMS_HIP(h, hipMemcpyAsync(dT, T[1], S * 8, hipMemcpyDeviceToDevice, q));
+        return TGMS_OK;
+    };
+    static const bool no_graph = std::getenv("TGMS_NO_GRAPH") != nullptr;
+    if (no_graph) return body(st);
+    // launch-bound (K x groups small kernels): capture once, replay while nothing changed
+    tgms_handle::LoopKey key{B, iters, d_so, dW, dT, T[1], dED, dC, d_cost, dSt, h->d_perm, k_T, eta,
+                             plan.counts, plan.starts, plan.uniform_m};
+    if (!(h->loop_exec && h->loop_key == key)) {
+        if (h->loop_exec) {
+            TGMS_HIP(h, hipGraphExecDestroy(h->loop_exec));
+            h->loop_exec = nullptr;
+        }
+        if (!h->cap_stream) TGMS_HIP(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+        s = ensure_aux(h);  // no stream/event creation inside the capture
+        if (s != TGMS_OK) return s;
+        TGMS_HIP(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        const tgms_status r = body(h->cap_stream);
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(h->cap_stream, &g);
+        if (r != TGMS_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return r;
+        }
+        if (e != hipSuccess) return hip_err(h, e, "hipStreamEndCapture");
+        const hipError_t ei = hipGraphInstantiate(&h->loop_exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ei != hipSuccess) {
+            h->loop_exec = nullptr;
+            return hip_err(h, ei, "hipGraphInstantiate");
+        }
+        h->loop_key = key;
+    }
+    TGMS_HIP(h, hipGraphLaunch(h->loop_exec, st));
     return TGMS_OK;
 }
 

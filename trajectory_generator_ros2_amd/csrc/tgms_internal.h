@@ -34,6 +34,21 @@ hipError_t launch_refine_ragged_group(int M, int32_t n, const int32_t* perm, con
                                       const double* W, const double* T, const double* ED, double kT, double eta,
                                       double* Tout, double* cost, int32_t* status, hipStream_t stream);
 
+// Several M groups of a ragged batch in one launch.  Group g owns wavefronts
+// [blk_end[g-1], blk_end[g]) and its n[g] trajectories perm[g][0..n) have m[g] segments.
+// cls 0 takes M in 1..11 (two waves per SIMD), cls 1 M in 12..16 (one wave per SIMD).
+constexpr int RAGGED_TPW = 32;  // trajectories per wavefront of the reduced kernels
+struct GroupTable {
+    int32_t ngroups;
+    int32_t m[16];
+    int32_t n[16];
+    int32_t blk_end[16];
+    const int32_t* perm[16];
+};
+hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* seg_offsets,
+                               const double* W, const double* T, const double* ED, double kT, double eta,
+                               double* Tout, double* cost, double* C, int32_t* status, hipStream_t stream);
+
 // Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,
                          const double* ED, const double* C, double dt, int yaw_mode,

@@ -1822,21 +1822,20 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_uniform(int32_t B,
     if (live && !right && status) status[b] = st;
 }
 
+// One wavefront of a ragged group: trajectories perm[blk*TPW ...] (all with M segments).
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_ragged(int32_t n, const int32_t* __restrict__ perm,
-                                                                      const int32_t* __restrict__ seg_offsets,
-                                                                      const double* __restrict__ W,
-                                                                      const double* __restrict__ T,
-                                                                      const double* __restrict__ ED, double kT,
-                                                                      double eta, double* __restrict__ Tout,
-                                                                      double* __restrict__ cost,
-                                                                      int32_t* __restrict__ status) {
+__device__ __forceinline__ void refine_ragged_block(Stage<M>& sm, int64_t blk, int32_t n,
+                                                    const int32_t* __restrict__ perm,
+                                                    const int32_t* __restrict__ seg_offsets,
+                                                    const double* __restrict__ W, const double* __restrict__ T,
+                                                    const double* __restrict__ ED, double kT, double eta,
+                                                    double* __restrict__ Tout, double* __restrict__ cost,
+                                                    int32_t* __restrict__ status) {
     constexpr int NW = (M + 1) * 3;
-    __shared__ Stage<M> sm;
     const int lane = threadIdx.x;
     const int slot = lane >> 1;
     const bool right = lane & 1;
-    const int64_t i0 = (int64_t)blockIdx.x * TPW;
+    const int64_t i0 = blk * TPW;
     const int nb = (int)((n - i0) < TPW ? (n - i0) : TPW);
     const bool live = slot < nb;
     if (lane < TPW) sm.in.bad[lane] = 0;
@@ -1864,21 +1863,32 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_ragged(int32_t n, 
     if (live && !right && status) status[b] = st;
 }
 
-// Ragged batches: one launch per segment count M over the trajectories `perm`.
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
-                                                                       const int32_t* __restrict__ seg_offsets,
-                                                                       const double* __restrict__ W,
-                                                                       const double* __restrict__ T,
-                                                                       const double* __restrict__ ED,
-                                                                       double* __restrict__ C,
-                                                                       int32_t* __restrict__ status) {
-    constexpr int NW = (M + 1) * 3;
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_ragged(int32_t n, const int32_t* __restrict__ perm,
+                                                                      const int32_t* __restrict__ seg_offsets,
+                                                                      const double* __restrict__ W,
+                                                                      const double* __restrict__ T,
+                                                                      const double* __restrict__ ED, double kT,
+                                                                      double eta, double* __restrict__ Tout,
+                                                                      double* __restrict__ cost,
+                                                                      int32_t* __restrict__ status) {
     __shared__ Stage<M> sm;
+    refine_ragged_block<M, HAS_ED>(sm, blockIdx.x, n, perm, seg_offsets, W, T, ED, kT, eta, Tout, cost, status);
+}
+
+// Ragged batches: one wavefront = TPW trajectories of one segment count M (`perm`).
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, int32_t n,
+                                                     const int32_t* __restrict__ perm,
+                                                     const int32_t* __restrict__ seg_offsets,
+                                                     const double* __restrict__ W, const double* __restrict__ T,
+                                                     const double* __restrict__ ED, double* __restrict__ C,
+                                                     int32_t* __restrict__ status) {
+    constexpr int NW = (M + 1) * 3;
     const int lane = threadIdx.x;
     const int slot = lane >> 1;
     const bool right = lane & 1;
-    const int64_t i0 = (int64_t)blockIdx.x * TPW;
+    const int64_t i0 = blk * TPW;
     const int nb = (int)((n - i0) < TPW ? (n - i0) : TPW);
     const bool live = slot < nb;
     if (lane < TPW) {
@@ -1904,6 +1914,98 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n,
     const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
     const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, O);
     if (live && !right && status) status[b] = st;
+}
+
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
+                                                                       const int32_t* __restrict__ seg_offsets,
+                                                                       const double* __restrict__ W,
+                                                                       const double* __restrict__ T,
+                                                                       const double* __restrict__ ED,
+                                                                       double* __restrict__ C,
+                                                                       int32_t* __restrict__ status) {
+    __shared__ Stage<M> sm;
+    reduced_ragged_block<M, HAS_ED>(sm, blockIdx.x, n, perm, seg_offsets, W, T, ED, C, status);
+}
+
+// Every M group of a ragged plan in ONE launch (one per occupancy class: M <= 11 at
+// two waves per SIMD, M >= 12 at one): wavefront ranges [blk_end[g-1], blk_end[g])
+// belong to group g, longest groups first.  The groups then share the machine at
+// once instead of running one small grid after another.
+static_assert(TPW == RAGGED_TPW, "host group tables assume TPW trajectories per wavefront");
+
+template <int MLO, int MHI>
+constexpr size_t max_stage_bytes() {
+    size_t b = 0;
+#define TGMS_STAGE_MAX(m) \
+    if constexpr (m >= MLO && m <= MHI) b = b > sizeof(Stage<m>) ? b : sizeof(Stage<m>);
+    TGMS_STAGE_MAX(1) TGMS_STAGE_MAX(2) TGMS_STAGE_MAX(3) TGMS_STAGE_MAX(4) TGMS_STAGE_MAX(5) TGMS_STAGE_MAX(6)
+    TGMS_STAGE_MAX(7) TGMS_STAGE_MAX(8) TGMS_STAGE_MAX(9) TGMS_STAGE_MAX(10) TGMS_STAGE_MAX(11)
+    TGMS_STAGE_MAX(12) TGMS_STAGE_MAX(13) TGMS_STAGE_MAX(14) TGMS_STAGE_MAX(15) TGMS_STAGE_MAX(16)
+#undef TGMS_STAGE_MAX
+    return b;
+}
+
+__device__ __forceinline__ int group_of(const GroupTable& tab, int64_t bid, int64_t& blk) {
+    int g = 0;
+    while (g + 1 < tab.ngroups && bid >= tab.blk_end[g]) ++g;  // uniform, <= 16 steps
+    blk = bid - (g ? tab.blk_end[g - 1] : 0);
+    return g;
+}
+
+template <int MLO, int MHI, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_reduced_multi(GroupTable tab,
+                                                                        const int32_t* __restrict__ seg_offsets,
+                                                                        const double* __restrict__ W,
+                                                                        const double* __restrict__ T,
+                                                                        const double* __restrict__ ED,
+                                                                        double* __restrict__ C,
+                                                                        int32_t* __restrict__ status) {
+    __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
+    int64_t blk;
+    const int g = group_of(tab, blockIdx.x, blk);
+    switch (tab.m[g]) {
+#define TGMS_MULTI_CASE(mm)                                                                                \
+    case mm:                                                                                              \
+        if constexpr (mm >= MLO && mm <= MHI)                                                             \
+            reduced_ragged_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g], \
+                                             seg_offsets, W, T, ED, C, status);                           \
+        break;
+        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
+        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
+        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
+        TGMS_MULTI_CASE(16)
+#undef TGMS_MULTI_CASE
+        default: break;
+    }
+}
+
+template <int MLO, int MHI, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_multi(GroupTable tab,
+                                                                       const int32_t* __restrict__ seg_offsets,
+                                                                       const double* __restrict__ W,
+                                                                       const double* __restrict__ T,
+                                                                       const double* __restrict__ ED, double kT,
+                                                                       double eta, double* __restrict__ Tout,
+                                                                       double* __restrict__ cost,
+                                                                       int32_t* __restrict__ status) {
+    __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
+    int64_t blk;
+    const int g = group_of(tab, blockIdx.x, blk);
+    switch (tab.m[g]) {
+#define TGMS_MULTI_CASE(mm)                                                                                 \
+    case mm:                                                                                               \
+        if constexpr (mm >= MLO && mm <= MHI)                                                              \
+            refine_ragged_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g], \
+                                            seg_offsets, W, T, ED, kT, eta, Tout, cost, status);           \
+        break;
+        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
+        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
+        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
+        TGMS_MULTI_CASE(16)
+#undef TGMS_MULTI_CASE
+        default: break;
+    }
 }
 
 // The pipelined kernel needs both groups' inputs in LDS with 4 waves per CU
@@ -1980,7 +2082,39 @@ hipError_t refine_ragged_M(int32_t n, const int32_t* perm, const int32_t* so, co
     return hipGetLastError();
 }
 
+template <int MLO, int MHI>
+hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, const double* W, const double* T,
+                        const double* ED, double kT, double eta, double* Tout, double* cost, double* C,
+                        int32_t* status, hipStream_t stream) {
+    if (tab.ngroups <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)tab.blk_end[tab.ngroups - 1];
+    if (grid == 0) return hipSuccess;
+    if (refine) {
+        if (ED)
+            hipLaunchKernelGGL((k_refine_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
+                               kT, eta, Tout, cost, status);
+        else
+            hipLaunchKernelGGL((k_refine_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
+                               kT, eta, Tout, cost, status);
+    } else {
+        if (ED)
+            hipLaunchKernelGGL((k_reduced_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+                               ED, C, status);
+        else
+            hipLaunchKernelGGL((k_reduced_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+                               ED, C, status);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
+                               const double* T, const double* ED, double kT, double eta, double* Tout, double* cost,
+                               double* C, int32_t* status, hipStream_t stream) {
+    if (cls == 0) return multi_launch<1, 11>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    return multi_launch<12, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+}
 
 #ifdef TGMS_ONLY_M  // compile-only experiments: instantiate a single M
 #define TGMS_CASES(X) X(TGMS_ONLY_M)
