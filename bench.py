@@ -123,6 +123,82 @@ def config5_line(solver, B, dev, stream, iters=10, k_T=1.0, eta=0.1, reps=3):
             "k_T": k_T, "eta": eta}
 
 
+def config4_line(solver, M, dev, stream, world, rank, B=131072, chunks=8, reps=3):
+    """Config 4 (1,048,576 goals over 8 GPUs): every rank solves its 131,072-trajectory
+    shard (seed + rank) and the coefficients are gathered to rank 0 over RCCL, piece by
+    piece while the next piece is solved (shard.pipelined_gather).  Also reports the
+    solve alone at this size: 297 MB per launch, beyond the 256 MB Infinity Cache, so
+    it is the HBM-resident rate of the kernel.  At N = 1 there is nothing to gather."""
+    import torch
+    import torch.distributed as dist
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd import synthetic as S
+    _, W, T = S.uniform_batch(B, M, seed=S.SEED + rank)
+    dW = torch.from_numpy(W).to(dev)
+    dT = torch.from_numpy(T).to(dev)
+    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev)
+    dS = torch.zeros((B,), dtype=torch.int32, device=dev)
+    sp = stream.cuda_stream
+
+    def solve_chunk(lo, hi):
+        solver.solve_uniform_device(hi - lo, M, dW[lo:hi], dT[lo:hi], dC[lo:hi], dS[lo:hi], stream=sp)
+
+    # solve alone (kernel rate beyond the Infinity Cache)
+    solve_chunk(0, B)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        solve_chunk(0, B)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    solve_ms = e0.elapsed_time(e1) / reps
+    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+    line = {"workload": f"config4: {B} trajectories/GPU x {M} segments ({world * B} total), "
+                        f"coefficients gathered to rank 0",
+            "solve_ms": solve_ms,
+            "solve_GBs": algorithmic_bytes_per_traj(M) * B / (solve_ms * 1e-3) / 1e9}
+    if world == 1:
+        line["gather"] = None
+        return line
+
+    out = torch.empty((world, B, M, 3, 8), dtype=torch.float64, device=dev) if rank == 0 else None
+
+    def run():
+        for w in SH.pipelined_gather(solve_chunk, dC, chunks, dst=0, out=out):
+            w.wait()
+        torch.cuda.synchronize()
+
+    run()
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ts.append(float(t.item()))
+    ms = sorted(ts)[len(ts) // 2] * 1e3
+    if rank == 0:
+        # the gathered shards are the other ranks' solves: re-solve a slice of each
+        # rank's inputs here and compare bit for bit (same kernel, same inputs)
+        n = 1024
+        chk = torch.empty((n, M, 3, 8), dtype=torch.float64, device=dev)
+        for r in range(world):
+            _, Wr, Tr = S.uniform_batch(B, M, seed=S.SEED + r)
+            solver.solve_uniform_device(n, M, torch.from_numpy(Wr[:n]).to(dev), torch.from_numpy(Tr[:n]).to(dev),
+                                        chk, None, stream=sp)
+            torch.cuda.synchronize()
+            assert torch.equal(chk, out[r, :n]), f"gathered shard of rank {r} differs"
+    gathered = (world - 1) * B * M * 24 * 8
+    line["gather"] = {"collective": "torch.distributed.gather (RCCL send/recv) per piece, overlapped with the solve",
+                      "pieces": chunks, "ms_total": ms, "trajectories_per_s": world * B / (ms * 1e-3),
+                      "bytes_into_rank0": gathered, "rank0_ingest_GBs": gathered / (ms * 1e-3) / 1e9}
+    return line
+
+
 def host_line(solver, B, M, W, T, reps=3):
     """PCIe-inclusive rate: tgms_solve_batch on host buffers (H2D, solve, D2H), the call
     the node makes; reported beside `value`, never as it (SURVEY.md 8(d) timing)."""
@@ -192,6 +268,8 @@ def main():
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
     ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
+    ap.add_argument("--config4", type=int, default=1,
+                    help="config-4 side line (131,072/GPU, pipelined RCCL gather to rank 0 when N > 1): 1/0")
     ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     args = ap.parse_args()
@@ -284,6 +362,10 @@ def main():
     if args.config5 and M == 10:
         config5 = config5_line(solver, B, dev, stream)
 
+    config4 = None
+    if args.config4 and M == 10:
+        config4 = config4_line(solver, M, dev, stream, world, rank)
+
     sampler = None
     if args.sample_traj > 0:
         sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
@@ -329,6 +411,7 @@ def main():
             "cpu_baseline": cpu,
             "dense_kkt": dense,
             "sampler": sampler,
+            "config4": config4,
             "config5": config5,
             "host_path": host,
         }

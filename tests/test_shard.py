@@ -96,3 +96,52 @@ def test_gloo_world2_shard_and_gather(ragged, oracle):
         assert p.exitcode == 0
     res = [q.get(timeout=5) for _ in range(2)]
     assert all(res)
+
+
+def _pipelined_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, M = 203, 4
+        so, W, T = S.uniform_batch(B, M, seed=S.SEED + rank)
+        C = torch.zeros((B, M, 3, 8), dtype=torch.float64)
+
+        def solve_chunk(lo, hi):
+            c, st = O.solve_batch(so[lo:hi + 1] - so[lo], W[lo:hi].reshape(-1, 3), T[lo:hi].reshape(-1), None,
+                                  O.KKT_C4, 1)
+            assert (st == 0).all()
+            C[lo:hi] = torch.from_numpy(c.reshape(hi - lo, M, 3, 8))
+
+        out = torch.full((world, B, M, 3, 8), float("nan"), dtype=torch.float64) if rank == 0 else None
+        for w in SH.pipelined_gather(solve_chunk, C, chunks=5, dst=0, out=out):
+            w.wait()
+        if rank == 0:
+            ok = True
+            for r in range(world):
+                so_r, W_r, T_r = S.uniform_batch(B, M, seed=S.SEED + r)
+                ref, _ = O.solve_batch(so_r, W_r.reshape(-1, 3), T_r.reshape(-1), None, O.KKT_C4, 1)
+                ok &= np.array_equal(out[r].numpy().reshape(-1, 3, 8), ref)
+            q.put(bool(ok))
+        else:
+            q.put(True)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_pipelined_gather(oracle):
+    """bench.py's config-4 line: chunked solve + per-chunk gather to rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert all(q.get(timeout=5) for _ in range(2))

@@ -299,6 +299,113 @@ __device__ __forceinline__ void stage_axis(const OutBuf& o, const double (&c)[8]
 #endif
 }
 
+// Line-major output (uniform batches, even M; experiment, built with -DTGMS_LINES).
+// Beyond the Infinity Cache the HBM
+// write rate depends on whether the two 64-B halves of a 128-B line leave in the
+// same or in consecutive store instructions (scripts/storebench.hip, B = 524,288:
+// whole lines 5.5 TB/s; halves 4 instructions apart 3.9 TB/s; one axis per pass,
+// as the axis-sequential emission writes them, 3.4 TB/s).  A line of the
+// [traj][seg][axis][8] layout always holds two different axes, so the lines are
+// written after all three axes are solved: each lane computes the two rows of its
+// next line (its own rows in the virtual frame: the odd lane counts rows from the
+// trajectory's end), stages them as one 128-B LDS row, and every store
+// instruction writes 8 whole lines.  With 3M/2 lines per trajectory each lane owns
+// 3M/4 of them; for M = 2 mod 4 the middle line is shared (one row from each lane).
+template <int M>
+struct LineStage {
+    static constexpr int NLINE = 3 * M / 2;     // 128-B lines per trajectory
+    static constexpr int NFULL = (3 * M) / 4;   // whole lines per lane
+    static constexpr bool HALF = (3 * M) % 4 != 0;
+    alignas(16) double O[W64 * 16];             // one 128-B line per lane, 16-B chunks XOR-swizzled
+    RawIn<M> in;
+};
+
+struct OutLines {
+    double* stage;                  // LDS [W64][16] doubles
+    __amdgpu_buffer_rsrc_t rs;      // the wave's output block (range = its live trajectories)
+    uint32_t voff0;                 // byte offset of the lane's piece, line step 0, instruction 0
+    int32_t lstep;                  // +-128 B per line step
+    uint32_t voffh;                 // byte offset of the lane's piece of the middle line
+    uint32_t traj_b;                // bytes per trajectory
+    int lane;
+};
+
+template <int M>
+__device__ __forceinline__ OutLines make_out_lines(double* stage, double* C, int64_t b0, int nb, int lane) {
+    constexpr int TRAJ_B = M * 24 * 8;
+    constexpr int NLINE = LineStage<M>::NLINE;
+    OutLines o;
+    o.stage = stage;
+    o.lane = lane;
+    o.traj_b = TRAJ_B;
+    double* base = C + b0 * (M * 24);
+    const int block = nb * TRAJ_B;
+    o.rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, block, 0x00020000);
+    const bool side = (lane >> 3) & 1;  // the line was staged by an odd (right) lane
+    o.voff0 = (uint32_t)((lane >> 4) * TRAJ_B + (side ? (NLINE - 1) * 128 : 0) + (lane & 7) * 16);
+    o.lstep = side ? -128 : 128;
+    // middle line (M = 2 mod 4): instruction q covers trajectories 8q .. 8q+7
+    o.voffh = (uint32_t)((lane >> 3) * TRAJ_B + ((NLINE - 1) / 2) * 128 + (lane & 7) * 16);
+    return o;
+}
+
+__device__ __forceinline__ void stage_chunk(double* row, int c, int lane, double x, double y) {
+    *reinterpret_cast<double2*>(row + ((c ^ (lane & 7)) << 1)) = make_double2(x, y);
+}
+
+// Stage the lane's line (c0 = first half, c1 = second half in memory order) and
+// store 8 whole lines per instruction.
+__device__ __forceinline__ void store_line(const OutLines& o, const double (&c0)[8], const double (&c1)[8],
+                                           uint32_t voff) {
+    wave_lds_sync();  // previous readers are done with the stage
+    double* row = o.stage + o.lane * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stage_chunk(row, j, o.lane, c0[2 * j], c0[2 * j + 1]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stage_chunk(row, 4 + j, o.lane, c1[2 * j], c1[2 * j + 1]);
+    wave_lds_sync();
+    double2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int p = 8 * q + (o.lane >> 3), c = o.lane & 7;
+        v[q] = *reinterpret_cast<const double2*>(o.stage + p * 16 + ((c ^ (p & 7)) << 1));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#ifndef TGMS_ABL_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[q]), o.rs, voff + q * 4 * o.traj_b, 0,
+                                               TGMS_STORE_CPOL);
+#else
+        asm volatile("" ::"v"(v[q].x), "v"(voff));
+#endif
+    }
+}
+
+// The middle line of M = 2 mod 4: the even lane's last row is its first half, the
+// odd lane's last row its second half; 32 lines, 4 instructions.
+__device__ __forceinline__ void store_half(const OutLines& o, const double (&c)[8]) {
+    wave_lds_sync();
+    double* row = o.stage + o.lane * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) stage_chunk(row, j, o.lane, c[2 * j], c[2 * j + 1]);
+    wave_lds_sync();
+    double2 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int t = 8 * q + (o.lane >> 3), k = o.lane & 7, p = 2 * t + (k >> 2);
+        v[q] = *reinterpret_cast<const double2*>(o.stage + p * 16 + (((k & 3) ^ (p & 7)) << 1));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#ifndef TGMS_ABL_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[q]), o.rs, o.voffh + q * 8 * o.traj_b, 0,
+                                               TGMS_STORE_CPOL);
+#else
+        asm volatile("" ::"v"(v[q].x));
+#endif
+    }
+}
+
 // Output address of emission step e for either output context.
 __device__ __forceinline__ uint32_t out_step(const OutBuf& o, int e) { return o.voff0 + e * o.estep; }
 __device__ __forceinline__ int out_step(const OutCtx&, int e) { return e; }
@@ -859,6 +966,32 @@ __device__ __forceinline__ void seg_cost(double D, const double (&z)[6], double&
     Qd = qd;
 }
 
+// Coefficients of axis a of virtual segment e (virtual knots e, e+1 with derivatives
+// xs, xe of that axis), physical order c0..c7.
+__device__ __forceinline__ void row_coeffs(const LaneView& L, bool right, int e, int a, const double (&xs)[3],
+                                           const double (&xe)[3], double (&c)[8]) {
+    const double ws = L.w(e, a), we = L.w(e + 1, a);
+    const double w0 = right ? we : ws, w1 = right ? ws : we;
+    const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
+    const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
+    const double r = L.r(e);
+    const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
+    const double D = (w1 - w0) * r3;
+    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
+    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
+    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
+    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
+    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+    c[0] = w0;
+    c[1] = v0;
+    c[2] = 0.5 * a0;
+    c[3] = j0 * (1.0 / 6.0);
+    c[4] = P4 * r;
+    c[5] = P5 * r2;
+    c[6] = P6 * r3;
+    c[7] = P7 * r4;
+}
+
 template <int M, class Out>
 __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
                                           const double (&xs)[3], const double (&xe)[3], bool has_r) {
@@ -1197,6 +1330,202 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     }
 #endif
     MARK(ax_end);
+    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
+    const double fin_pair = fin + pair_swap(fin);
+    if (!valid) return TGMS_ERR_INVALID_ARG;
+    if (!spd_pair) return TGMS_ERR_SINGULAR;
+    if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
+    return TGMS_OK;
+}
+
+// One axis of the axis-sequential solve without emission: forward substitution,
+// interface, back substitution.  On return Y[s] = virtual knot s+1 and u0 = the
+// virtual start derivatives (same arithmetic as pair_solve_ax's axis loop).
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void axis_solve(const AxFactors<M>& Fa, const LaneView& L, bool right, int a, bool valid,
+                                           const double* __restrict__ ed, double (&u0)[3],
+                                           double (&Y)[Chain<M>::NS + 1][3], double& fin) {
+    using CH = Chain<M>;
+    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS;
+    const int nl = right ? nR : nL;
+    const double sg = right ? -1.0 : 1.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
+        const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
+        u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
+    }
+    {
+        double pp[8];
+        rpowers(L.r(0), pp);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            SCHED_FENCE();
+            const int k = s + 1;
+            double pn[8];
+            rpowers(L.r(k), pn);
+            double y[3];
+            knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
+            if (s >= 1) {
+                double B[3][3], v0, v1, v2;
+                coupling(pp, B);
+                ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
+            }
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Y[s][d] = y[d];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+        }
+    }
+    SCHED_FENCE();
+    double xm[3];
+    {
+        double yL[3], yR[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double yv = (nR > nL) ? (right ? Y[NS - 1][d] : Y[nL - 1][d]) : Y[nL - 1][d];
+            const double yp = (d == 1) ? yv : sg * yv;
+            yL[d] = pair_even(yp);
+            yR[d] = pair_odd(yp);
+        }
+        double Cc[3][3];
+        {
+            double pc[8];
+            rpowers(L.r(nl), pc);
+            coupling(pc, Cc);
+        }
+        double g0, g1, g2;
+        ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
+        double xc0, xc1, xc2, x10, x11, x12;
+        ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
+        const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
+        const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
+        const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
+        ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
+        xm[0] = right ? -x10 : xc0;
+        xm[1] = right ? x11 : xc1;
+        xm[2] = right ? -x12 : xc2;
+        const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
+        if (nR > nL) {
+            Y[nL][0] = right ? Y[nL][0] : o0;
+            Y[nL][1] = right ? Y[nL][1] : o1;
+            Y[nL][2] = right ? Y[nL][2] : o2;
+            Y[nR][0] = right ? o0 : Y[nR][0];
+            Y[nR][1] = right ? o1 : Y[nR][1];
+            Y[nR][2] = right ? o2 : Y[nR][2];
+        } else {
+            Y[nL][0] = o0;
+            Y[nL][1] = o1;
+            Y[nL][2] = o2;
+        }
+        fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
+    }
+#pragma unroll
+    for (int s = NS - 1; s >= 0; --s) {
+        SCHED_FENCE();
+        const bool at_end = (s == nl - 1);
+        const bool inside = (s < nl - 1);
+        if (s + 1 < NS) {
+            double B[3][3];
+            {
+                double pb[8];
+                rpowers(L.r(s + 1), pb);
+                coupling(pb, B);
+            }
+            double b[3], x0, x1, x2;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) b[d] = Y[s][d] - (B[d][0] * Y[s + 1][0] + B[d][1] * Y[s + 1][1] + B[d][2] * Y[s + 1][2]);
+            ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
+            Y[s][0] = at_end ? xm[0] : (inside ? x0 : Y[s][0]);
+            Y[s][1] = at_end ? xm[1] : (inside ? x1 : Y[s][1]);
+            Y[s][2] = at_end ? xm[2] : (inside ? x2 : Y[s][2]);
+            fin += inside ? (x0 + x1) + x2 : 0.0;
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
+        }
+    }
+}
+
+// Coefficients of the lane's virtual row q (0 .. 3M/2-1): virtual segment q / 3,
+// axis q % 3 on the even lane and 2 - q % 3 on the odd lane, whose rows run from
+// the trajectory's end (physical row 3M-1-q).
+template <int M>
+__device__ __forceinline__ void lane_row(const LaneView& L, bool right, int q, const double (&u0)[3][3],
+                                         const double (&Y)[3][Chain<M>::NS + 1][3], double (&c)[8]) {
+    const int e = q / 3, slot = q % 3;
+    double xs[3], xe[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const double s_a = (e == 0) ? u0[slot][d] : Y[slot][e >= 1 ? e - 1 : 0][d];
+        const double s_b = (e == 0) ? u0[2 - slot][d] : Y[2 - slot][e >= 1 ? e - 1 : 0][d];
+        xs[d] = right ? s_b : s_a;
+        xe[d] = right ? Y[2 - slot][e][d] : Y[slot][e][d];
+    }
+    row_coeffs(L, right, e, right ? 2 - slot : slot, xs, xe, c);
+}
+
+// Axis-sequential solve of all three axes, then line-major emission (even M).
+template <int M, bool HAS_ED, class V>
+__device__ __forceinline__ int32_t pair_solve_lines(const LaneView& L, bool right, V&& valid_src,
+                                                    const double* __restrict__ ed, const OutLines& O) {
+    using CH = Chain<M>;
+    using LS = LineStage<M>;
+    static_assert(M % 2 == 0 && M >= 4, "line-major emission needs even M >= 4");
+    static_assert(CH::NE == CH::NS && CH::nR == CH::NS, "even M: both lanes emit NS segments");
+    constexpr int NS = CH::NS;
+    AxFactors<M> Fa;
+    ax_factor<M>(Fa, L, right);
+    const bool valid = get_valid(valid_src);
+    double fin = 0.0;
+    double u0[3][3];
+    double Y[3][NS + 1][3];
+    axis_solve<M, HAS_ED>(Fa, L, right, 0, valid, ed, u0[0], Y[0], fin);
+    // the line stage is idle until the emission: park axis 0's knot data there
+    // ([value][lane], conflict-free) while the other two axes are solved (the
+    // two-wave builds; one wave per SIMD has the registers)
+    constexpr bool PARK = NS * 3 <= 16 && TGMS_WAVES(M) == 2;
+    SCHED_FENCE();
+    if constexpr (PARK) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) O.stage[(s * 3 + d) * W64 + O.lane] = Y[0][s][d];
+    }
+    axis_solve<M, HAS_ED>(Fa, L, right, 1, valid, ed, u0[1], Y[1], fin);
+    axis_solve<M, HAS_ED>(Fa, L, right, 2, valid, ed, u0[2], Y[2], fin);
+    SCHED_FENCE();
+    if constexpr (PARK) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Y[0][s][d] = O.stage[(s * 3 + d) * W64 + O.lane];
+    }
+    MARK(lines);
+#pragma unroll
+    for (int k = 0; k < LS::NFULL; ++k) {
+        SCHED_FENCE();
+        double r0[8], r1[8];
+        lane_row<M>(L, right, 2 * k, u0, Y, r0);
+        lane_row<M>(L, right, 2 * k + 1, u0, Y, r1);
+        double h0[8], h1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            h0[j] = right ? r1[j] : r0[j];
+            h1[j] = right ? r0[j] : r1[j];
+        }
+        store_line(O, h0, h1, O.voff0 + k * O.lstep);
+    }
+    if constexpr (LS::HALF) {
+        SCHED_FENCE();
+        double r0[8];
+        lane_row<M>(L, right, 2 * LS::NFULL, u0, Y, r0);
+        store_half(O, r0);
+    }
     const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
@@ -1617,7 +1946,12 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
                                                                         const double* __restrict__ ED,
                                                                         double* __restrict__ C,
                                                                         int32_t* __restrict__ status) {
-    __shared__ RawStage<M> sm;
+#ifdef TGMS_LINES  // experiment: line-major emission (see LineStage; slower at config 3)
+    constexpr bool LINES = (M % 2 == 0) && M >= 4;
+#else
+    constexpr bool LINES = false;
+#endif
+    __shared__ std::conditional_t<LINES, LineStage<M>, RawStage<M>> sm;
     STAMP_RT(6);
     STAMP(0);
     const int lane = threadIdx.x;
@@ -1639,8 +1973,14 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
         return !any_bad || sm.in.bad[slot] == 0;
     };
     const LaneView L = make_view_raw<M>(sm.in, slot, right);
-    const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane);
-    const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    int32_t st;
+    if constexpr (LINES) {
+        const OutLines O = make_out_lines<M>(sm.O, C, b0, nb, lane);
+        st = pair_solve_lines<M, HAS_ED>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    } else {
+        const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane);
+        st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    }
     STAMP(5);
     STAMP_RT(7);
     if (live && !right && status) status[b] = st;

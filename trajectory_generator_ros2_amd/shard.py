@@ -117,3 +117,36 @@ class ShardedBatch:
         Call = torch.cat([cl[r][: int(seg_per_rank[r])] for r in range(self.world)])
         Sall = torch.cat([sl[r][: int(traj_per_rank[r])] for r in range(self.world)])
         return Call.reshape(-1, 3, 8), Sall
+
+
+def pipelined_gather(solve_chunk: Callable, coeffs, chunks: int, dst: int = 0, out=None, group=None):
+    """Solve this rank's uniform shard in `chunks` pieces and gather every piece to
+    rank `dst` while the next one is being solved (the final
+    coefficient gather, overlapped with the compute in chunks).
+
+    coeffs   this rank's [B, ...] coefficient tensor (every rank the same B)
+    solve_chunk(lo, hi)  enqueues the solve of trajectories [lo, hi) into coeffs[lo:hi]
+             on the current stream (GPU) or computes it (CPU tests)
+    out      on rank dst: a [world, B, ...] tensor that receives every rank's shard in
+             rank order (rank-major = global trajectory order for contiguous shards);
+             ignored elsewhere
+
+    Each piece is one torch.distributed.gather (ncclSend/ncclRecv under RCCL, issued
+    on the communicator's stream after the piece's solve), so the transfer of piece
+    c runs beside the solve of piece c + 1.  Returns the list of async works (the
+    caller waits on them)."""
+    import torch.distributed as dist
+
+    B = coeffs.shape[0]
+    world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    bounds = uniform_bounds(B, max(1, chunks))
+    works = []
+    for c in range(len(bounds) - 1):
+        lo, hi = int(bounds[c]), int(bounds[c + 1])
+        if hi <= lo:
+            continue
+        solve_chunk(lo, hi)
+        gl = [out[r, lo:hi] for r in range(world)] if me == dst else None
+        works.append(dist.gather(coeffs[lo:hi], gl, dst=dst, group=group, async_op=True))
+    return works
