@@ -2,6 +2,7 @@
 # kbench.py over batch sizes (in and beyond the 256 MB Infinity Cache) for the default
 # build and every variant under lib/variants
 set -u
+shopt -s nullglob
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/bsweep
 for B in ${BS:-65536 131072 262144 524288}; do
