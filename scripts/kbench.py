@@ -31,7 +31,12 @@ else:
     from oracle import oracle as O
     R, _ = O.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, O.KKT_C4, 16)
     R = R.reshape(B, M, 3, 8); np.save(ref_path, R)
-err = float((np.abs(C - R).max(axis=(1, 3)) / np.abs(R).max(axis=(1, 3))).max())
+errs = np.abs(C - R).max(axis=(1, 3)) / np.abs(R).max(axis=(1, 3))
+err = float(errs.max())
+bad = np.argwhere(errs > 1e-9)
+if len(bad):
+    print(json.dumps({"n_bad": int(len(bad)), "first_bad": bad[:8].tolist(),
+                      "worst": np.unravel_index(int(errs.argmax()), errs.shape)[0].item()}), file=sys.stderr)
 print(json.dumps({"lib": os.path.basename(os.environ.get("TGMS_LIB", "default")), "B": B, "M": M,
                   "median_us": ms[K // 2] * 1e3, "min_us": ms[0] * 1e3,
                   "traj_per_s": B / (ms[K // 2] * 1e-3), "max_rel_err": err,
