@@ -25,6 +25,8 @@
  *     src/trajectory_generator_node.cpp:30);
  *   - `*_device` entry points take device pointers and a hipStream_t passed as
  *     void* and are asynchronous; the others take host pointers and block;
+ *     fp64 device arrays must be 16-byte aligned (TGMS_ERR_INVALID_ARG otherwise;
+ *     hipMalloc allocations are, a slice at an odd element offset is not);
  *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
  *     TGMS_ERR_NO_DEVICE.
  *

@@ -11,5 +11,7 @@ for B in ${BS:-65536 131072 262144 524288}; do
     if [ $so = default ]; then unset TGMS_LIB; else export TGMS_LIB=$PWD/$so; fi
     KB_B=$B timeout -k 10 120 python3 scripts/kbench.py > gpurun_out/bsweep/${n}_$B.json 2>gpurun_out/bsweep/${n}_$B.err; c=$?
     cat gpurun_out/bsweep/${n}_$B.json; [ $c -eq 0 ] || exit $c
+    KB_ROT=4 KB_B=$B timeout -k 10 120 python3 scripts/kbench.py > gpurun_out/bsweep/${n}_${B}_rot.json 2>gpurun_out/bsweep/${n}_${B}_rot.err; c=$?
+    cat gpurun_out/bsweep/${n}_${B}_rot.json; [ $c -eq 0 ] || exit $c
   done
 done

@@ -19,8 +19,18 @@ for _ in range(3):
     s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
 torch.cuda.synchronize()
 e0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]; e1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+ROT = int(os.environ.get("KB_ROT", 1))  # >1: a fresh batch every launch (beyond the Infinity Cache)
+sets = [(dW, dT, dC)]
+for i in range(1, ROT):
+    _, Wi, Ti = S.uniform_batch(B, M, seed=S.SEED + 1000 + i)
+    sets.append((torch.from_numpy(Wi).cuda(), torch.from_numpy(Ti).cuda(), torch.empty_like(dC)))
+for k in range(ROT):
+    s.solve_uniform_device(B, M, *sets[k][:2], sets[k][2], dS, stream=sp)
 for k in range(K):
-    e0[k].record(); s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp); e1[k].record()
+    a, b_, c_ = sets[k % ROT]
+    e0[k].record(); s.solve_uniform_device(B, M, a, b_, c_, dS, stream=sp); e1[k].record()
+torch.cuda.synchronize()
+s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
 torch.cuda.synchronize()
 ms = sorted(e0[k].elapsed_time(e1[k]) for k in range(K))
 C = dC.cpu().numpy()
@@ -37,7 +47,7 @@ bad = np.argwhere(errs > 1e-9)
 if len(bad):
     print(json.dumps({"n_bad": int(len(bad)), "first_bad": bad[:8].tolist(),
                       "worst": np.unravel_index(int(errs.argmax()), errs.shape)[0].item()}), file=sys.stderr)
-print(json.dumps({"lib": os.path.basename(os.environ.get("TGMS_LIB", "default")), "B": B, "M": M,
+print(json.dumps({"lib": os.path.basename(os.environ.get("TGMS_LIB", "default")), "B": B, "M": M, "rot": ROT,
                   "median_us": ms[K // 2] * 1e3, "min_us": ms[0] * 1e3,
                   "traj_per_s": B / (ms[K // 2] * 1e-3), "max_rel_err": err,
                   "status_ok": bool((dS == 0).all().item())}))

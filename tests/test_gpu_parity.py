@@ -339,3 +339,28 @@ def test_refine_loop_device_matches_host(solver):
     np.testing.assert_array_equal(dC.cpu().numpy(), Ch)
     np.testing.assert_array_equal(dcost.cpu().numpy(), ch)
     assert int(dst.abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_device_slices_and_alignment(solver):
+    """bench.py's config-4 line solves a batch piece by piece through slices of the
+    device arrays: aligned slices give the unsliced result bit for bit; a slice at an
+    odd element offset (8-B aligned only) is refused before any launch."""
+    import torch
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, TgmsError
+    from trajectory_generator_ros2_amd import synthetic as S
+    B, M = 4096, 10
+    _, W, T = S.uniform_batch(B, M, seed=11)
+    dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+    full = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+    solver.solve_uniform_device(B, M, dW, dT, full)
+    pieces = torch.full_like(full, float("nan"))
+    bounds = [0, 64, 1026, 2050, 4096]  # even trajectory offsets: every slice 16-B aligned
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        solver.solve_uniform_device(hi - lo, M, dW[lo:hi], dT[lo:hi], pieces[lo:hi])
+    torch.cuda.synchronize()
+    assert torch.equal(full, pieces)
+    odd = dW.reshape(-1)[1:1 + 100 * (M + 1) * 3]  # 8 bytes past a 16-B boundary
+    with pytest.raises(TgmsError) as e:
+        solver.solve_uniform_device(100, M, odd, dT[:100], full[:100])
+    assert e.value.status == ERR_INVALID_ARG and "aligned" in solver.last_error()

@@ -6,6 +6,7 @@
 // MinSnap adapter maps a failure to the reference's RCLCPP_ERROR + exit(1)
 // (Line.cpp:77-78).  There is deliberately NO CPU fallback: without a HIP
 // device tgms_create() fails with TGMS_ERR_NO_DEVICE.
+#include <initializer_list>
 #include "tgms.h"
 #include "tgms_internal.h"
 
@@ -422,6 +423,20 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
     return (tgms_status)worst;
 }
 
+// Device buffers: the kernels move fp64 data in 16-B pieces (double2 loads/stores,
+// buffer_store_b128), so every fp64 device array must be 16-byte aligned (hipMalloc
+// and torch allocations are 256-B aligned; a slice at an odd element offset is not).
+static bool misaligned(std::initializer_list<const void*> ps) {
+    for (const void* p : ps)
+        if (p && (reinterpret_cast<uintptr_t>(p) & 15u)) return true;
+    return false;
+}
+#define TGMS_CHECK_ALIGNED(h, ...)                                                                   \
+    do {                                                                                             \
+        if (misaligned({__VA_ARGS__}))                                                               \
+            return set_err(h, TGMS_ERR_INVALID_ARG, "fp64 device buffers must be 16-byte aligned"); \
+    } while (0)
+
 tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* dW,
                                       const double* dT, const double* dED, double* dC,
                                       int32_t* dSt, void* stream) {
@@ -432,6 +447,7 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, cons
                        "bad B or M for this method");
     if (B == 0) return TGMS_OK;
     if (!dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (h->method == TGMS_METHOD_REDUCED)
         TGMS_HIP(h, tgms::launch_reduced_uniform(M, B, dW, dT, dED, dC, dSt, st));
@@ -449,6 +465,7 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
     Plan plan;
     s = make_plan(h, B, h_so, max_m_for(h), &plan, static_cast<hipStream_t>(stream));
     if (s != TGMS_OK) return s;
@@ -465,6 +482,7 @@ tgms_status tgms_refine_uniform_device(tgms_handle* h, int32_t B, int32_t M, con
     if (B < 0 || M < 1 || M > TGMS_MAX_SEGMENTS) return set_err(h, TGMS_ERR_INVALID_ARG, "bad B or M");
     if (B == 0) return TGMS_OK;
     if (!dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dT_out, d_cost);
     TGMS_HIP(h, tgms::launch_refine_uniform(M, B, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
                                             static_cast<hipStream_t>(stream)));
     return TGMS_OK;
@@ -481,6 +499,7 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dT_out, d_cost);
     Plan plan;
     s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, static_cast<hipStream_t>(stream));
     if (s != TGMS_OK) return s;
@@ -561,6 +580,7 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t S = (size_t)h_so[B];
     s = ensure_ws(h, align256(S * 8));
@@ -643,6 +663,7 @@ tgms_status tgms_sample_batch_device(tgms_handle* h, int32_t B, const int32_t* d
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC || !d_sample_offsets || !d_out)
         return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_out);
     TGMS_HIP(h, tgms::launch_sample(B, d_so, dW, dT, dED, dC, dt, yaw_mode, yaw_const, d_sample_offsets,
                                     d_out, static_cast<hipStream_t>(stream)));
     return TGMS_OK;
