@@ -87,8 +87,14 @@ def cpu_baseline(B: int, M: int, target_s: float):
     t1 = time.perf_counter()
     O.solve_batch(so[:2049], W[:2048], T[:2048], None, O.KKT_C4, 1)
     one_core = 2048 / (time.perf_counter() - t1)
+    # the same threads on the reduced formulation (the GPU kernel's math, O(M) per
+    # trajectory): the strongest CPU restatement, beside the survey's dense-KKT one
+    t2 = time.perf_counter()
+    _, st = O.solve_batch(so, W, T, None, O.REDUCED, threads)
+    assert (st == 0).all()
+    reduced = B / (time.perf_counter() - t2)
     return {"value": n / el, "unit": "trajectories/s", "cores": threads, "kind": "port",
-            "value_1core": one_core, "cpu_model": _cpu_model(),
+            "value_1core": one_core, "value_reduced_formulation": reduced, "cpu_model": _cpu_model(),
             "sample": f"{reps} x {n_batch} trajectories of the config-3 workload (M={M}), oracle dense KKT "
                       f"(LU, partial pivoting, fp64), {threads} OpenMP thread(s), {el:.1f} s"}
 
@@ -235,6 +241,50 @@ def rotating_line(solver, B, M, dev, stream, sets=4, K=40):
             "trajectories_per_s": B / (ms * 1e-3), "achieved_GBs": gbs, "frac_of_peak": gbs / HBM_PEAK_GBS}
 
 
+def node_line(reps=20):
+    """Config 1 through the node's own path: one goal of 4 waypoints (3 segments) from
+    parameters to a sampled 100 Hz Goal stream — MinSnap::readParameters (validation +
+    tgms_solve_batch, B = 1) then generateTraj (tgms_sample_batch + append), the
+    calls TrajectoryGenerator makes at start-up (src/TrajectoryGenerator.cpp:54, :71).
+    Beside it the CPU oracle's solve + sample of the same goal (1 core)."""
+    from oracle import oracle as O
+    from trajectory_generator_ros2_amd.node import MinSnapNode
+    wp = [0.0, 0.0, 1.0, 2.0, 1.0, 1.5, 3.0, -1.0, 2.0, 0.5, -2.0, 1.0]
+    st = [2.0, 2.0, 2.5]
+    params = {"alt": 1.8, "pub_freq": 100.0, "traj_type": "MinSnap", "waypoints": wp, "seg_times": st,
+              "yaw_mode": "constant", "yaw": 0.0, "stop_accel": 1.0, "x_min": -5.0, "x_max": 5.0,
+              "y_min": -5.0, "y_max": 5.0, "z_min": -5.0, "z_max": 5.0}
+    ts, n_goals = [], 0
+    for _ in range(reps + 2):
+        t0 = time.perf_counter()
+        n = MinSnapNode(params)
+        assert n.read_parameters()
+        n_goals = n.generate_traj()
+        ts.append(time.perf_counter() - t0)
+        n.close()
+    gpu_ms = sorted(ts[2:])[reps // 2] * 1e3
+    n = MinSnapNode(params)
+    assert n.read_parameters()
+    n.generate_traj()
+    tw = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        n.generate_traj()
+        tw.append(time.perf_counter() - t0)
+    n.close()
+    W, T = np.array(wp).reshape(-1, 3), np.array(st)
+    tc = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        R, s = O.solve(W, T)
+        O.sample(R, T, W, None, 0.01)
+        tc.append(time.perf_counter() - t0)
+    return {"workload": "config1: 1 goal, 4 waypoints, 3 segments, sampled at 100 Hz (650 goals)",
+            "goals": n_goals, "ms_params_to_goals": gpu_ms,
+            "ms_generate_traj_warm": sorted(tw)[reps // 2] * 1e3,
+            "cpu_oracle_ms_solve_and_sample": sorted(tc)[reps // 2] * 1e3}
+
+
 def host_line(solver, B, M, W, T, reps=3):
     """PCIe-inclusive rate: tgms_solve_batch on host buffers (H2D, solve, D2H), the call
     the node makes; reported beside `value`, never as it (SURVEY.md 8(d) timing)."""
@@ -308,6 +358,7 @@ def main():
                     help="side line: a fresh batch every launch (4 batches, beyond the Infinity Cache): 1/0")
     ap.add_argument("--config4", type=int, default=1,
                     help="config-4 side line (131,072/GPU, pipelined RCCL gather to rank 0 when N > 1): 1/0")
+    ap.add_argument("--node-line", type=int, default=1, help="config-1 node-path latency side line: 1/0")
     ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     args = ap.parse_args()
@@ -416,6 +467,10 @@ def main():
     if args.host_line and rank == 0:
         host = host_line(solver, B, M, W, T)
 
+    node = None
+    if args.node_line and rank == 0:
+        node = node_line()
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(B, M, args.cpu_seconds)
@@ -457,6 +512,7 @@ def main():
             "config4": config4,
             "config5": config5,
             "host_path": host,
+            "node_config1": node,
         }
         print(json.dumps(line), flush=True)
     solver.close()
