@@ -246,15 +246,18 @@ struct OutBuf {
     uint32_t voff0;                 // byte offset of the lane's piece, emission step 0, axis 0
     int32_t estep;                  // +-1 segment (192 B) per emission step
     bool rt;                        // the lane's pieces were staged by odd (right) lanes
+    bool nt;                        // streaming stores (the batch's output exceeds the Infinity Cache)
     int lane;
 };
 
 template <int M>
-__device__ __forceinline__ OutBuf make_out_buf(double* stage, double* C, int64_t b0, int nb, int lane) {
+__device__ __forceinline__ OutBuf make_out_buf(double* stage, double* C, int64_t b0, int nb, int lane,
+                                               bool nt = false) {
     constexpr int TRAJ_B = M * 24 * 8;  // bytes per trajectory
     OutBuf o;
     o.stage = stage;
     o.lane = lane;
+    o.nt = nt;
     double* base = C + b0 * (M * 24);
     const int block = nb * TRAJ_B;
 #pragma unroll
@@ -270,9 +273,17 @@ __device__ __forceinline__ OutBuf make_out_buf(double* stage, double* C, int64_t
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#ifndef TGMS_STORE_CPOL  // cache policy of the coefficient stores (gfx950: sc0 = 1, nt = 2, sc1 = 16)
-#define TGMS_STORE_CPOL 16  // sc1: measured 28.2 -> 26.9 us; nt (streaming) 41 us
+// Cache policy of the coefficient stores (gfx950: sc0 = 1, nt = 2, sc1 = 16).  A batch
+// whose output stays in the 256 MB Infinity Cache (config 3: 126 MB) wants sc1
+// (28.2 -> 26.9 us; nt 41 us there); one whose output does not (config 4's 131,072
+// per GPU: 252 MB) wants sc1|nt (92 -> 74 us with a fresh batch every launch).
+#ifndef TGMS_STORE_CPOL
+#define TGMS_STORE_CPOL 16
 #endif
+#ifndef TGMS_STORE_CPOL_NT
+#define TGMS_STORE_CPOL_NT 18
+#endif
+constexpr int64_t kStreamingOutputBytes = 192ll << 20;
 
 // Stage one axis of every lane's current segment, then store it (OutBuf version;
 // `voff` is the lane's piece offset at this emission step).
@@ -290,10 +301,17 @@ __device__ __forceinline__ void stage_axis(const OutBuf& o, const double (&c)[8]
     const double2 v0 = piece(0), v1 = piece(1), v2 = piece(2), v3 = piece(3);
     const uint32_t off = (has_r || !o.rt) ? voff : 0x80000000u;  // idle odd rows: out of range
 #ifndef TGMS_ABL_NOSTORE
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), o.rs[0], off, a * 64, TGMS_STORE_CPOL);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), o.rs[1], off, a * 64, TGMS_STORE_CPOL);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v2), o.rs[2], off, a * 64, TGMS_STORE_CPOL);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v3), o.rs[3], off, a * 64, TGMS_STORE_CPOL);
+    if (o.nt) {  // wave-uniform
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), o.rs[0], off, a * 64, TGMS_STORE_CPOL_NT);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), o.rs[1], off, a * 64, TGMS_STORE_CPOL_NT);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v2), o.rs[2], off, a * 64, TGMS_STORE_CPOL_NT);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v3), o.rs[3], off, a * 64, TGMS_STORE_CPOL_NT);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), o.rs[0], off, a * 64, TGMS_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), o.rs[1], off, a * 64, TGMS_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v2), o.rs[2], off, a * 64, TGMS_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v3), o.rs[3], off, a * 64, TGMS_STORE_CPOL);
+    }
 #else
     asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"(v2.x), "v"(v3.x), "v"(off));
 #endif
@@ -1945,7 +1963,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
                                                                         const double* __restrict__ T,
                                                                         const double* __restrict__ ED,
                                                                         double* __restrict__ C,
-                                                                        int32_t* __restrict__ status) {
+                                                                        int32_t* __restrict__ status, int nt) {
 #ifdef TGMS_LINES  // experiment: line-major emission (see LineStage; slower at config 3)
     constexpr bool LINES = (M % 2 == 0) && M >= 4;
 #else
@@ -1978,7 +1996,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
         const OutLines O = make_out_lines<M>(sm.O, C, b0, nb, lane);
         st = pair_solve_lines<M, HAS_ED>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
     } else {
-        const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane);
+        const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane, nt != 0);
         st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
     }
     STAMP(5);
@@ -2372,10 +2390,13 @@ hipError_t uniform_M(int32_t B, const double* W, const double* T, const double* 
             hipLaunchKernelGGL((k_reduced_pipe<M, false>), dim3(g2), dim3(W64), 0, stream, B, W, T, ED, C, status);
         return hipGetLastError();
     }
+    const int nt = (int64_t)B * M * 24 * 8 > kStreamingOutputBytes;
     if (ED)
-        hipLaunchKernelGGL((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status);
+        hipLaunchKernelGGL((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
+                           nt);
     else
-        hipLaunchKernelGGL((k_reduced_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status);
+        hipLaunchKernelGGL((k_reduced_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
+                           nt);
     return hipGetLastError();
 }
 
