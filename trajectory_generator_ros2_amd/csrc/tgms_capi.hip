@@ -204,10 +204,9 @@ tgms_status run_parallel(tgms_handle* h, hipStream_t stream,
 
 // Reduced method, ragged plan: every M group in one launch per occupancy class
 // (M <= 11 / M >= 12), the longest groups' wavefronts first.
-tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, bool refine, const int32_t* d_so,
-                             const double* W, const double* T, const double* ED, double kT, double eta,
-                             double* Tout, double* cost, double* C, int32_t* st) {
-    tgms::GroupTable tab[2] = {};
+void class_tables(const tgms_handle* h, const Plan& p, tgms::GroupTable (&tab)[2]) {
+    tab[0] = tgms::GroupTable{};
+    tab[1] = tgms::GroupTable{};
     for (size_t m = p.counts.size(); m-- > 1;) {
         if (!p.counts[m]) continue;
         tgms::GroupTable& t = tab[m >= 12 ? 1 : 0];
@@ -217,6 +216,13 @@ tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, 
         t.perm[g] = h->d_perm + p.starts[m];
         t.blk_end[g] = (g ? t.blk_end[g - 1] : 0) + (p.counts[m] + tgms::RAGGED_TPW - 1) / tgms::RAGGED_TPW;
     }
+}
+
+tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, bool refine, const int32_t* d_so,
+                             const double* W, const double* T, const double* ED, double kT, double eta,
+                             double* Tout, double* cost, double* C, int32_t* st) {
+    tgms::GroupTable tab[2];
+    class_tables(h, p, tab);
     std::vector<std::function<hipError_t(hipStream_t)>> jobs;
     for (int c = 1; c >= 0; --c)
         if (tab[c].ngroups)
@@ -265,6 +271,38 @@ tgms_status dispatch_refine(tgms_handle* h, const Plan& p, int32_t B, const int3
 tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
                         double* const T[2], const double* ED, double kT, double eta, int32_t iters, double* C,
                         double* cost, int32_t* st, hipStream_t stream, int* cur) {
+    if (B > 0 && p.uniform_m == 0) {
+        // Ragged: the two occupancy classes hold disjoint trajectories, so each runs its
+        // whole chain (steps, cost, final solve) on its own stream and they meet once at
+        // the end; neither waits for the other's step (each class alone fills ~2/3 of
+        // the GPU).
+        tgms::GroupTable tab[2];
+        class_tables(h, p, tab);
+        std::vector<std::function<hipError_t(hipStream_t)>> jobs;
+        for (int k = 1; k >= 0; --k)
+            if (tab[k].ngroups)
+                jobs.push_back([&, k](hipStream_t q) -> hipError_t {
+                    int c = 0;
+                    for (int32_t it = 0; it < iters; ++it, c ^= 1) {
+                        const hipError_t e = tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, eta,
+                                                                       T[c ^ 1], nullptr, nullptr, st, q);
+                        if (e != hipSuccess) return e;
+                    }
+                    if (cost) {
+                        const hipError_t e = tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, 0.0,
+                                                                       T[c ^ 1], cost, nullptr, st, q);
+                        if (e != hipSuccess) return e;
+                    }
+                    if (C)
+                        return tgms::launch_ragged_multi(k, tab[k], false, d_so, W, T[c], ED, 0.0, 0.0, nullptr,
+                                                         nullptr, C, st, q);
+                    return hipSuccess;
+                });
+        tgms_status s = run_parallel(h, stream, jobs);
+        if (s != TGMS_OK) return s;
+        *cur = iters & 1;
+        return TGMS_OK;
+    }
     int c = 0;
     for (int32_t k = 0; k < iters; ++k, c ^= 1) {
         tgms_status s = dispatch_refine(h, p, B, d_so, W, T[c], ED, kT, eta, T[c ^ 1], nullptr, st, stream);
