@@ -209,7 +209,7 @@ void class_tables(const tgms_handle* h, const Plan& p, tgms::GroupTable (&tab)[2
     tab[1] = tgms::GroupTable{};
     for (size_t m = p.counts.size(); m-- > 1;) {
         if (!p.counts[m]) continue;
-        tgms::GroupTable& t = tab[m >= 12 ? 1 : 0];
+        tgms::GroupTable& t = tab[m > TGMS_TWO_WAVE_MAX_M ? 1 : 0];
         const int g = t.ngroups++;
         t.m[g] = (int32_t)m;
         t.n[g] = p.counts[m];

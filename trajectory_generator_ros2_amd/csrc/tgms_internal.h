@@ -6,6 +6,12 @@
 
 namespace tgms {
 
+// Largest M solved at two wavefronts per SIMD (the axis-sequential state of larger M
+// needs more than 256 registers); ragged batches launch one kernel per class.
+#ifndef TGMS_TWO_WAVE_MAX_M
+#define TGMS_TWO_WAVE_MAX_M 11
+#endif
+
 // Reduced-Hessian solve, uniform M (configs 2-4).  Grid: ceil(B/64) waves.
 hipError_t launch_reduced_uniform(int M, int32_t B, const double* W, const double* T,
                                   const double* ED, double* C, int32_t* status,

@@ -39,7 +39,7 @@ namespace {
 #ifdef TGMS_MIN_WAVES
 #define TGMS_WAVES(M) TGMS_MIN_WAVES
 #else
-#define TGMS_WAVES(M) ((M) <= 11 ? 2 : 1)
+#define TGMS_WAVES(M) ((M) <= TGMS_TWO_WAVE_MAX_M ? 2 : 1)
 #endif
 
 // Scheduling fence between unrolled chain / emission steps.  The compiler-level
@@ -2473,8 +2473,9 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
                                const double* T, const double* ED, double kT, double eta, double* Tout, double* cost,
                                double* C, int32_t* status, hipStream_t stream) {
-    if (cls == 0) return multi_launch<1, 11>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
-    return multi_launch<12, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    if (cls == 0)
+        return multi_launch<1, TGMS_TWO_WAVE_MAX_M>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    return multi_launch<TGMS_TWO_WAVE_MAX_M + 1, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
 }
 
 #ifdef TGMS_ONLY_M  // compile-only experiments: instantiate a single M
