@@ -34,6 +34,14 @@ def algorithmic_bytes_per_traj(M: int, with_status: bool = True) -> int:
     return (M + 1) * 3 * 8 + M * 8 + M * 24 * 8 + (4 if with_status else 0)
 
 
+def band_flops_per_traj(M: int) -> float:
+    """GEPP flops that touch the band of the interleaved KKT (kl = 9, U width 19) with
+    3 right-hand sides: per column 9 multipliers + 9 x (18 + 3) updates, then back
+    substitution over 18 super-diagonals x 3 axes."""
+    N = 14 * M + 2
+    return N * (9 + 2 * 9 * 21) + N * 3 * 2 * 18
+
+
 def dense_flops_per_traj(M: int) -> float:
     N = 14 * M + 2
     return 2.0 / 3.0 * N ** 3 + 6.0 * N ** 2
@@ -351,6 +359,7 @@ def main():
     ap.add_argument("--segments", type=int, default=10)
     ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
     ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
+    ap.add_argument("--band-steps", type=int, default=5, help="steps of the band-KKT side line (0: skip)")
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
     ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
@@ -375,7 +384,7 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    from trajectory_generator_ros2_amd import METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
     from trajectory_generator_ros2_amd import synthetic as S
     from trajectory_generator_ros2_amd.solver import Solver
 
@@ -447,6 +456,29 @@ def main():
                  "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
 
+    # band-KKT side line: the same literal KKT and partial-pivoting LU in the order in
+    # which it is banded (tgms_band.hip), same inputs, same GPU
+    band = None
+    if args.band_steps > 0 and args.method == "reduced":
+        solver.set_method(METHOD_BAND_KKT)
+        dC3 = torch.empty_like(dC)
+        solver.solve_uniform_device(B, M, dW, dT, dC3, dS, stream=sp)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.band_steps):
+            solver.solve_uniform_device(B, M, dW, dT, dC3, dS, stream=sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        assert int((dS != 0).sum().item()) == 0, "band KKT reported failures"
+        bms = e0.elapsed_time(e1) / args.band_steps
+        diff = (dC3 - dC).abs().amax(dim=(1, 3)) / dC.abs().amax(dim=(1, 3)).clamp_min(1e-300)
+        band = {"value": B / (bms * 1e-3) * world, "ms_per_step": bms,
+                "fp64_tflops_algorithmic": band_flops_per_traj(M) * B / (bms * 1e-3) / 1e12,
+                "flops_per_traj": band_flops_per_traj(M), "fp64_peak_tflops": FP64_PEAK_TFS,
+                "max_rel_diff_vs_reduced": float(diff.max().item())}
+        solver.set_method(METHOD_REDUCED)
+
     config5 = None
     if args.config5 and M == 10:
         config5 = config5_line(solver, B, dev, stream)
@@ -507,6 +539,7 @@ def main():
                          "algorithmic_bytes_per_launch": bpl},
             "cpu_baseline": cpu,
             "dense_kkt": dense,
+            "band_kkt": band,
             "sampler": sampler,
             "rotating_batches": rotating,
             "config4": config4,

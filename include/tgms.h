@@ -67,8 +67,12 @@ typedef enum tgms_status {
 typedef enum tgms_method {
     TGMS_METHOD_REDUCED = 0,  /* default: Schur complement of the KKT onto the free knot
                                  derivatives, block-tridiagonal LDL^T, one lane per trajectory */
-    TGMS_METHOD_DENSE_KKT = 1 /* the survey's literal a1-a3: KKT assembled in LDS, partial-
-                                 pivoting LU, one wavefront per trajectory */
+    TGMS_METHOD_DENSE_KKT = 1, /* the survey's literal a1-a3: KKT assembled in LDS, partial-
+                                 pivoting LU, one workgroup per trajectory (M <= 10) */
+    TGMS_METHOD_BAND_KKT = 2   /* the same KKT and LU with partial pivoting, in the
+                                 segment-interleaved order where it is banded (kl = ku = 9);
+                                 the structurally-zero entries are skipped, half a wavefront
+                                 per trajectory, M <= TGMS_MAX_SEGMENTS */
 } tgms_method;
 
 typedef enum tgms_yaw_mode {

@@ -392,6 +392,42 @@ static int solve_reduced(int M, const double* W, const double* T, const double* 
 
 /* ------------------------------------------------------------------ driver */
 
+/* Position of KKT_C4 row/column q in the segment-interleaved order
+ *   [start rows (4) | c_0 (8) | knot-1 rows (6) | c_1 (8) | ... | c_{M-1} (8) | end rows (4)]
+ * in which every nonzero lies within 9 of the diagonal. */
+static int interleaved_pos(int M, int q) {
+    const int n = 8 * M;
+    if (q < n) return 4 + 14 * (q / 8) + q % 8;  /* coefficient j of segment i */
+    const int r = q - n;
+    if (r < 4) return r;                          /* start rows */
+    if (r < 8) return 14 * M - 2 + (r - 4);       /* end rows */
+    const int i = (r - 8) / 6, t = (r - 8) % 6;   /* knot after segment i */
+    return 4 + 14 * i + 8 + t;
+}
+
+/* Dense GEPP of the permuted KKT: the same algorithm (lu_solve) the band kernel
+ * performs, which skips only entries that are structurally zero in this order. */
+static int solve_kkt_interleaved(int M, const double* W, const double* T, const double* ED, double* C) {
+    const int N = 14 * M + 2;
+    double* K = scratch((size_t)2 * N * N + (size_t)2 * N * 3);
+    if (!K) return ORACLE_INVALID;
+    double* rhs = K + (size_t)N * N;
+    double* P = rhs + (size_t)N * 3;
+    double* prhs = P + (size_t)N * N;
+    assemble_kkt_cont(M, 4, W, T, ED, K, rhs);
+    for (int q = 0; q < N; ++q) {
+        const int pq = interleaved_pos(M, q);
+        for (int s = 0; s < N; ++s) P[(size_t)pq * N + interleaved_pos(M, s)] = K[(size_t)q * N + s];
+        for (int a = 0; a < 3; ++a) prhs[pq * 3 + a] = rhs[q * 3 + a];
+    }
+    int st = lu_solve(N, P, 3, prhs);
+    if (st == ORACLE_OK)
+        for (int i = 0; i < M; ++i)
+            for (int a = 0; a < 3; ++a)
+                for (int j = 0; j < 8; ++j) C[(i * 3 + a) * 8 + j] = prhs[interleaved_pos(M, 8 * i + j) * 3 + a];
+    return st;
+}
+
 static int all_finite(const double* x, int n) {
     for (int i = 0; i < n; ++i)
         if (!isfinite(x[i])) return 0;
@@ -407,6 +443,7 @@ int oracle_solve(int formulation, int M, const double* W, const double* T, const
         case ORACLE_KKT_C3: st = solve_kkt(M, 3, W, T, ED, C); break;
         case ORACLE_SQUARE_C6: st = solve_square_c6(M, W, T, ED, C); break;
         case ORACLE_REDUCED: st = solve_reduced(M, W, T, ED, C); break;
+        case ORACLE_KKT_BAND: st = solve_kkt_interleaved(M, W, T, ED, C); break;
         default: return ORACLE_INVALID;
     }
     if (st == ORACLE_OK && !all_finite(C, 24 * M)) st = ORACLE_NONFINITE;

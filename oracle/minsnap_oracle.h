@@ -52,6 +52,8 @@ extern "C" {
 #define ORACLE_KKT_C3 1     /* same with continuity of d1..d3 only, N = 13M+3 */
 #define ORACLE_SQUARE_C6 2  /* square 8M system: interpolation + continuity of d1..d6 */
 #define ORACLE_REDUCED 3    /* reduced Hessian over free knot derivatives (v,a,j), dense Cholesky */
+#define ORACLE_KKT_BAND 4   /* the KKT_C4 matrix in segment-interleaved order, dense GEPP (the
+                               order in which it is banded; checker of TGMS_METHOD_BAND_KKT) */
 
 /* Solve one trajectory. Returns ORACLE_* status. */
 int oracle_solve(int formulation, int M, const double* waypoints, const double* seg_times,

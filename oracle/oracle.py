@@ -18,7 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-KKT_C4, KKT_C3, SQUARE_C6, REDUCED = 0, 1, 2, 3
+KKT_C4, KKT_C3, SQUARE_C6, REDUCED, KKT_BAND = 0, 1, 2, 3, 4
 YAW_CONSTANT, YAW_VELOCITY = 0, 1
 
 _lib = None

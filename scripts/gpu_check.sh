@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 ok() { local c=$1; [ "$c" -eq 0 ] || [ "$c" -eq 1 ]; }   # 1 = test failure, keep going
-SIDE_OFF="--dense-steps 0 --sample-traj 0 --config5 0 --config4 0 --rotating 0 --host-line 0 --node-line 0"
+SIDE_OFF="--dense-steps 0 --band-steps 0 --sample-traj 0 --config5 0 --config4 0 --rotating 0 --host-line 0 --node-line 0"
 
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; c=$?
 echo "pytest exit $c"; tail -5 $OUT/pytest_gpu.log

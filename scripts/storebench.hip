@@ -93,6 +93,31 @@ __global__ __launch_bounds__(64) void p8(double* C) {
     }
 }
 
+// P9: P5's axis-outer order, but the first write of every 128-B line is a whole line
+// (the row plus a placeholder for the partner row, back-to-back instructions), so the
+// line is valid on-die before its partner half arrives a pass later as a 64-B write.
+__global__ __launch_bounds__(64) void p9(double* C) {
+    double* base = C + (size_t)blockIdx.x * TPW * TRAJ;
+    const int lane = threadIdx.x;
+    for (int a = 0; a < 3; ++a)
+        for (int e = 0; e < M / 2; ++e) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int p = lane + 64 * q, chunk = p >> 2, off = p & 3, slot = chunk >> 1, rt = chunk & 1;
+                const int seg = rt ? (M - 1 - e) : e;
+                reinterpret_cast<double2*>(base + slot * TRAJ + seg * 24 + a * 8)[off] = val(e, a);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int p = lane + 64 * q, chunk = p >> 2, off = p & 3, slot = chunk >> 1, rt = chunk & 1;
+                const int seg = rt ? (M - 1 - e) : e;
+                const int r = seg * 3 + a, pr = r ^ 1, pa = pr % 3;
+                if (pa > a)  // partner row not yet written: fill its half now
+                    reinterpret_cast<double2*>(base + slot * TRAJ + pr * 8)[off] = val(-1, a);
+            }
+        }
+}
+
 // P2: direct per-lane stores: lane (slot, side) writes its 192-B segment as 12 x 16 B.
 __global__ __launch_bounds__(64) void p2(double* C) {
     double* base = C + (size_t)blockIdx.x * TPW * TRAJ;
@@ -138,11 +163,11 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    void (*ks[])(double*) = {p0, p1, p2, p3, p4, p5, p6, p7, p8<1>, p8<2>, p8<4>, p8<8>, p8<16>};
+    void (*ks[])(double*) = {p0, p1, p2, p3, p4, p5, p6, p7, p8<1>, p8<2>, p8<4>, p8<8>, p8<16>, p9};
     const char* names[] = {"P0 coalesced", "P1 axis-stage 64B", "P2 direct 16B/lane", "P3 seg-stage 192B",
-                           "P4 seg-pair 384B", "P5 axis-outer 64B", "P6 full lines 8/instr", "P7 half lines back-to-back", "P8 halves 1 apart", "P8 halves 2 apart", "P8 halves 4 apart", "P8 halves 8 apart", "P8 halves 16 apart"};
+                           "P4 seg-pair 384B", "P5 axis-outer 64B", "P6 full lines 8/instr", "P7 half lines back-to-back", "P8 halves 1 apart", "P8 halves 2 apart", "P8 halves 4 apart", "P8 halves 8 apart", "P8 halves 16 apart", "P9 axis-outer, first write whole line"};
     for (int occ = 0; occ < 1; ++occ) {
-        for (int k = 0; k < 13; ++k) {
+        for (int k = 0; k < 14; ++k) {
             for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(ks[k], dim3(NW), dim3(64), 0, 0, C);
             hipEventRecord(e0);
             for (int it = 0; it < 20; ++it) hipLaunchKernelGGL(ks[k], dim3(NW), dim3(64), 0, 0, C);

@@ -58,7 +58,7 @@ def test_hermite_cost_matrix_is_integer_and_psd():
 
 
 @pytest.mark.parametrize("path", GOLDENS, ids=[os.path.basename(p) for p in GOLDENS])
-@pytest.mark.parametrize("form", [0, 1, 2, 3], ids=["kkt_c4", "kkt_c3", "square_c6", "reduced"])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4], ids=["kkt_c4", "kkt_c3", "square_c6", "reduced", "kkt_band"])
 def test_oracle_vs_exact_goldens(oracle, path, form):
     g = np.load(path)
     so = g["seg_offsets"]
@@ -78,6 +78,37 @@ def test_kat_single_segment_closed_form(oracle):
                 ref = float(X.closed_form_single(W[0, a], W[1, a], T[0], t))
                 got = np.polyval(Cx[0, a, ::-1], t)
                 assert abs(got - ref) <= 1e-12 * (1 + abs(ref))
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 10, 16])
+def test_interleaved_kkt_is_banded(oracle, M):
+    """The order TGMS_METHOD_BAND_KKT eliminates in ([start | c_0 | knot 1 | c_1 | ... |
+    end]) puts every nonzero of the KKT within 9 of the diagonal, so GEPP keeps L in
+    9 sub-diagonals and U in 18 super-diagonals: the band kernel skips only zeros."""
+    from trajectory_generator_ros2_amd import synthetic as S
+    _, W, T = S.uniform_batch(1, M, seed=M)
+    K, _ = oracle.assemble_kkt(W[0], T[0])
+    n = 8 * M
+    order = list(range(n, n + 4))
+    for i in range(M):
+        order += list(range(8 * i, 8 * i + 8))
+        if i < M - 1:
+            order += list(range(n + 8 + 6 * i, n + 14 + 6 * i))
+    order += list(range(n + 4, n + 8))
+    assert sorted(order) == list(range(14 * M + 2))
+    P = K[np.ix_(order, order)]
+    r, c = np.nonzero(P)
+    assert np.abs(r - c).max() <= 9
+    # GEPP on the permuted matrix: no fill outside the band
+    A = P.copy()
+    N = A.shape[0]
+    for k in range(N):
+        p = k + int(np.argmax(np.abs(A[k:, k])))
+        A[[k, p]] = A[[p, k]]
+        A[k + 1:, k] /= A[k, k]
+        A[k + 1:, k + 1:] -= np.outer(A[k + 1:, k], A[k, k + 1:])
+        assert not A[k + 10:, k].any()
+    assert not np.triu(A, 19).any()
 
 
 def test_kkt_assembly_structure(oracle):

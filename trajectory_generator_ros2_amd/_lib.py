@@ -12,7 +12,7 @@ import os
 from .build import LIB_TGMS
 
 OK, ERR_INVALID_ARG, ERR_SINGULAR, ERR_NONFINITE, ERR_NO_DEVICE, ERR_DEVICE, ERR_UNSUPPORTED = range(7)
-METHOD_REDUCED, METHOD_DENSE_KKT = 0, 1
+METHOD_REDUCED, METHOD_DENSE_KKT, METHOD_BAND_KKT = 0, 1, 2
 YAW_CONSTANT, YAW_VELOCITY = 0, 1
 ABI_VERSION = 1
 MAX_SEGMENTS = 16

@@ -25,7 +25,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TGMS_ARCH", "gfx950")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 
-HIP_SOURCES = ["tgms_reduced.hip", "tgms_dense.hip", "tgms_sample.hip", "tgms_capi.hip"]
+HIP_SOURCES = ["tgms_reduced.hip", "tgms_dense.hip", "tgms_band.hip", "tgms_sample.hip", "tgms_capi.hip"]
 HOST_SOURCES = ["MinSnap.cpp", "factory.cpp", "tgms_node_capi.cpp"]
 
 

@@ -61,6 +61,10 @@ struct tgms_handle {
     } loop_key;
     hipGraphExec_t loop_exec = nullptr;
     hipStream_t cap_stream = nullptr;
+    // band-KKT method: persistent grid and the U slabs of its wavefronts (grow-only)
+    int32_t band_grid = 0;
+    double* d_band = nullptr;
+    size_t band_cap = 0;
 };
 
 namespace {
@@ -232,9 +236,52 @@ tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, 
     return run_parallel(h, stream, jobs);
 }
 
+#ifndef TGMS_BAND_WAVES_PER_CU
+#define TGMS_BAND_WAVES_PER_CU 16
+#endif
+
+// Band-KKT scratch for largest M `m_max`; the slabs are per wavefront of one launch,
+// so launches sharing them are serialised on one stream.
+tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream) {
+    if (h->band_grid == 0) {
+        int cus = 0;
+        TGMS_HIP(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+        h->band_grid = std::max(1, cus) * TGMS_BAND_WAVES_PER_CU;
+    }
+    const size_t need = tgms::band_scratch_bytes(m_max, h->band_grid);
+    if (need <= h->band_cap) return TGMS_OK;
+    if (h->d_band) {
+        TGMS_HIP(h, hipStreamSynchronize(stream));
+        TGMS_HIP(h, hipDeviceSynchronize());
+        TGMS_HIP(h, hipFree(h->d_band));
+        h->d_band = nullptr;
+        h->band_cap = 0;
+    }
+    TGMS_HIP(h, hipMalloc(&h->d_band, need));
+    h->band_cap = need;
+    return TGMS_OK;
+}
+
 tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
                      const double* T, const double* ED, double* C, int32_t* st, hipStream_t stream) {
     if (B == 0) return TGMS_OK;
+    if (h->method == TGMS_METHOD_BAND_KKT) {
+        int m_max = p.uniform_m;
+        for (size_t m = 1; m < p.counts.size(); ++m)
+            if (p.counts[m]) m_max = std::max(m_max, (int)m);
+        tgms_status s = ensure_band(h, m_max, stream);
+        if (s != TGMS_OK) return s;
+        if (p.uniform_m > 0) {
+            TGMS_HIP(h, tgms::launch_band_kkt(p.uniform_m, B, nullptr, nullptr, W, T, ED, C, st, h->d_band,
+                                              h->band_grid, stream));
+            return TGMS_OK;
+        }
+        for (size_t m = p.counts.size(); m-- > 1;)
+            if (p.counts[m])
+                TGMS_HIP(h, tgms::launch_band_kkt((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED, C,
+                                                  st, h->d_band, h->band_grid, stream));
+        return TGMS_OK;
+    }
     if (p.uniform_m > 0) {
         if (h->method == TGMS_METHOD_REDUCED)
             TGMS_HIP(h, tgms::launch_reduced_uniform(p.uniform_m, B, W, T, ED, C, st, stream));
@@ -375,6 +422,7 @@ void tgms_destroy(tgms_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     (void)hipDeviceSynchronize();
     if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->d_band) (void)hipFree(h->d_band);
     if (h->d_perm) (void)hipFree(h->d_perm);
     if (h->h_perm) (void)hipHostFree(h->h_perm);
     if (h->perm_ev) (void)hipEventDestroy(h->perm_ev);
@@ -393,7 +441,7 @@ const char* tgms_last_error(const tgms_handle* h) { return h ? h->last_error.c_s
 
 tgms_status tgms_set_method(tgms_handle* h, int method) {
     if (!h) return TGMS_ERR_INVALID_ARG;
-    if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT)
+    if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT && method != TGMS_METHOD_BAND_KKT)
         return set_err(h, TGMS_ERR_INVALID_ARG, "unknown method");
     h->method = method;
     return TGMS_OK;
@@ -487,7 +535,11 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, cons
     if (!dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (h->method == TGMS_METHOD_REDUCED)
+    if (h->method == TGMS_METHOD_BAND_KKT) {
+        tgms_status s = ensure_band(h, M, st);
+        if (s != TGMS_OK) return s;
+        TGMS_HIP(h, tgms::launch_band_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, h->d_band, h->band_grid, st));
+    } else if (h->method == TGMS_METHOD_REDUCED)
         TGMS_HIP(h, tgms::launch_reduced_uniform(M, B, dW, dT, dED, dC, dSt, st));
     else
         TGMS_HIP(h, tgms::launch_dense_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, st));

@@ -32,6 +32,15 @@ hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nul
                             const double* T, const double* ED, double* C, int32_t* status,
                             hipStream_t stream);
 
+// Band-KKT solve (the same KKT and partial-pivoting LU, segment-interleaved order, the
+// structurally-zero entries skipped): two trajectories per wavefront, persistent grid of
+// `grid` wavefronts, each with a private U slab in `scratch` (band_scratch_bytes).
+size_t band_scratch_bytes(int M, int32_t grid);
+hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nullable*/,
+                           const int32_t* seg_offsets /*nullable if uniform*/, const double* W,
+                           const double* T, const double* ED, double* C, int32_t* status, double* scratch,
+                           int32_t grid, hipStream_t stream);
+
 // Time-allocation refinement step (solve + snap-cost gradient + log-space step on T):
 // uniform batches, and one M group of a ragged batch.  Tout may not alias T.
 hipError_t launch_refine_uniform(int M, int32_t B, const double* W, const double* T, const double* ED, double kT,
