@@ -21,7 +21,7 @@
 // powers T_i^e and the 2Q blocks staged in LDS (a1/a2 never exist as a matrix).
 // Each finished U row (19 entries + 3 eliminated right-hand sides, 176 B) goes to a
 // per-wave scratch slab; back substitution streams the slab in reverse with loads
-// issued four steps ahead, one lane per pending row, x_k broadcast through LDS.
+// issued 16 steps ahead, one lane per pending row, x_k broadcast through LDS.
 #include <algorithm>
 
 #include "tgms_device.h"
@@ -35,7 +35,7 @@ constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
 constexpr int UW = WC + 3;         // scratch row: U row + 3 eliminated right-hand sides
 constexpr int HL = 32;             // lanes per trajectory
-constexpr int PF = 4;              // back-substitution prefetch depth (steps)
+constexpr int PFB = 16;            // back-substitution prefetch depth (steps)
 
 // Position q of the interleaved order.  kind: 0 start row (idx = derivative k),
 // 1 coefficient (seg, idx = power j), 2 interior-knot row after segment seg
@@ -66,89 +66,106 @@ __device__ __forceinline__ double dfac(int j, int k) {
     return (k > j) ? 0.0 : (double)f;
 }
 
-// A[lam][coefficient (i, j)], tp = this trajectory's T_i^e table
-template <int M>
-__device__ __forceinline__ double a_entry(Pos lam, int i, int j, const double* tp) {
-    if (lam.kind == 0) return (i == 0 && j == lam.idx) ? dfac(j, j) : 0.0;
-    if (lam.kind == 3)
-        return (i == M - 1 && j >= lam.idx) ? dfac(j, lam.idx) * tp[i * 8 + j - lam.idx] : 0.0;
-    if (lam.kind != 2) return 0.0;
-    const int s = lam.seg, t = lam.idx, k = t - 1;
-    if (i == s) {
-        if (t == 0) return tp[s * 8 + j];
-        if (t == 1 || j < k) return 0.0;
-        return dfac(j, k) * tp[s * 8 + j - k];
+// Entries of the interleaved KKT, framed in the block of segment i: offsets 0..7 are
+// c_i, 8..13 the rows of the knot after segment i (the end rows if i = M-1), -4..-1 the
+// start rows (i = 0).  Every entry is coef * V_i[idx] with V_i = [1, T_i^0..T_i^7,
+// 2Q_i (16)] staged per trajectory in LDS, and (coef, idx) depends only on the block
+// variant (first / last segment), the row offset o and the diagonal offset d = c - r, so
+// the pattern is a small table built once per wavefront: an entering row costs two LDS
+// reads per lane instead of a divergent case analysis.  Same entries as oracle
+// assemble_kkt_cont; tests/test_oracle.py pins the band.
+constexpr int VAL = 25;               // V_i stride
+constexpr int NOFF = 18;              // row offsets -4..13
+constexpr int NDESC = 4 * NOFF * WC;  // variants x offsets x diagonals
+
+__host__ __device__ constexpr int pack(int coef, int idx) { return coef * 32 + idx; }
+
+__device__ int desc_entry(int vv, int o, int d) {
+    const bool first = vv & 1, last = vv & 2;
+    if (o < 0 && !first) return 0;
+    const int oc = o + d;
+    auto at = [](int j, int kk) { return j >= kk ? pack((int)dfac(j, kk), 1 + j - kk) : 0; };
+    auto before = [](int j, int t) {  // knot row type t on the coefficients of the next segment
+        if (t == 0) return 0;
+        if (t == 1) return j == 0 ? pack(1, 0) : 0;
+        return j == t - 1 ? pack(-(int)dfac(j, j), 0) : 0;
+    };
+    if (o < 0) {  // start row k: r_k(0) on segment 0 = k! at coefficient k
+        const int k = o + 4;
+        return oc == k ? pack((int)dfac(k, k), 0) : 0;
     }
-    if (i == s + 1) {
-        if (t == 0) return 0.0;
-        if (t == 1) return (j == 0) ? 1.0 : 0.0;
-        return (j == k) ? -dfac(k, k) : 0.0;
+    if (o < 8) {  // stationarity row of coefficient j of segment i
+        const int j = o;
+        if (oc >= 0 && oc < 8) return (j >= 4 && oc >= 4) ? pack(1, 9 + (j - 4) * 4 + (oc - 4)) : 0;
+        if (oc >= 14) return 0;
+        if (oc >= 8) {
+            const int t = oc - 8;
+            if (last) return at(j, t);
+            return t == 1 ? 0 : at(j, t == 0 ? 0 : t - 1);
+        }
+        if (first) return (oc + 4 == j) ? pack((int)dfac(j, j), 0) : 0;
+        if (oc < -6) return 0;
+        return before(j, oc + 6);
     }
-    return 0.0;
+    const int t = o - 8;  // knot row after segment i (type t), or end row k = t
+    if (oc >= 0 && oc < 8) {
+        if (last) return at(oc, t);
+        return t == 1 ? 0 : at(oc, t == 0 ? 0 : t - 1);
+    }
+    if (!last && oc >= 14 && oc < 22) return before(oc - 14, t);
+    return 0;
 }
 
-// KKT entry K[r][c] of the interleaved order
-template <int M>
-__device__ __forceinline__ double kkt_entry(Pos r, Pos c, const double* tp, const double* q2) {
-    if (r.kind == 4 || c.kind == 4) return 0.0;
-    if (r.kind == 1 && c.kind == 1)
-        return (r.seg == c.seg && r.idx >= 4 && c.idx >= 4) ? q2[r.seg * 16 + (r.idx - 4) * 4 + (c.idx - 4)] : 0.0;
-    if (r.kind == 1) return a_entry<M>(c, r.seg, r.idx, tp);
-    if (c.kind == 1) return a_entry<M>(r, c.seg, c.idx, tp);
-    return 0.0;
-}
-
-// right-hand side of row r, axis a (0 on the stationarity rows)
+// Row r (wave-uniform) at this lane's column c; lanes WC..WC+2 return the right-hand
+// side b_r of axis hl - WC.
 template <int M, bool HAS_ED>
-__device__ __forceinline__ double kkt_rhs(Pos r, int a, const double* w, const double* ed) {
-    if (r.kind == 0) return r.idx == 0 ? w[a] : (HAS_ED ? ed[(r.idx - 1) * 3 + a] : 0.0);
-    if (r.kind == 3) return r.idx == 0 ? w[M * 3 + a] : (HAS_ED ? ed[9 + (r.idx - 1) * 3 + a] : 0.0);
-    if (r.kind == 2) return r.idx <= 1 ? w[(r.seg + 1) * 3 + a] : 0.0;
-    return 0.0;
+__device__ __forceinline__ double row_entry(int hl, int r, int c, const int* desc, const double* val,
+                                            const double* w, const double* ed) {
+    constexpr int N = 14 * M + 2;
+    if (r >= N || hl >= UW) return 0.0;
+    const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
+    const int o = r - (4 + 14 * i);
+    if (hl >= WC) {  // right-hand sides
+        const int a = hl - WC;
+        if (o < 0) return o == -4 ? w[a] : (HAS_ED ? ed[(o + 3) * 3 + a] : 0.0);
+        if (o < 8) return 0.0;
+        const int t = o - 8;
+        if (i == M - 1) return t == 0 ? w[M * 3 + a] : (HAS_ED ? ed[9 + (t - 1) * 3 + a] : 0.0);
+        return t <= 1 ? w[(i + 1) * 3 + a] : 0.0;
+    }
+    const int d = c - r;
+    if (c >= N || d < -KL || d > KL) return 0.0;
+    const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
+    const int de = desc[(vv * NOFF + o + 4) * WC + d + KL];
+    return (double)(de >> 5) * val[i * VAL + (de & 31)];
 }
 
-template <int M, bool HAS_ED>
-__device__ __forceinline__ double window_entry(int hl, int row, Pos pc, const double* tp, const double* q2,
-                                               const double* w, const double* ed) {
-    const Pos pr = decode<M>(row);
-    if (hl < WC) return kkt_entry<M>(pr, pc, tp, q2);
-    if (hl < UW) return kkt_rhs<M, HAS_ED>(pr, hl - WC, w, ed);
-    return 0.0;
+// 1/x: hardware reciprocal + two Newton steps (within an ulp; the pivots only scale)
+__device__ __forceinline__ double recip(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
 }
 
 // One elimination step k; logical window row i lives in a[(R0 + i) % WR].
 template <int M, bool HAS_ED, int R0>
-__device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR], int& col, Pos& pc, bool& sing,
-                                          double* slot, double* U, const double* tp, const double* q2,
+__device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR], int& col, bool& sing,
+                                          double* slot, double* U, const int* desc, const double* val,
                                           const double* w, const double* ed) {
 #define A_(i) a[(R0 + (i)) % WR]
-    // pivot search (meaningful on the pivot column's lane Lk)
+    // pivot search in every lane's own column; the pivot column's lane Lk decides
     double best = fabs(A_(0));
     int p = 0;
 #pragma unroll
     for (int i = 1; i < WR; ++i) {
         const double v = fabs(A_(i));
-        if (v > best) {
-            best = v;
-            p = i;
-        }
+        p = (v > best) ? i : p;
+        best = fmax(best, v);
     }
-    if (hl == Lk) {
-        double piv = A_(0);
-#pragma unroll
-        for (int i = 1; i < WR; ++i) piv = (p == i) ? A_(i) : piv;
-        sing = sing || !(best > 0.0);
-        const double rp = 1.0 / piv;
-        slot[0] = (double)p;
-#pragma unroll
-        for (int i = 1; i < WR; ++i) slot[i] = ((p == i) ? A_(0) : A_(i)) * rp;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int P = (int)slot[0];
-    double l[WR];
-#pragma unroll
-    for (int i = 1; i < WR; ++i) l[i] = slot[i];
-    // row interchange 0 <-> P, then the rank-1 update of the window
+    // the two halves' pivot rows (lanes Lk and Lk + 32) through the scalar unit
+    const int p0 = __builtin_amdgcn_readlane(p, Lk), p1 = __builtin_amdgcn_readlane(p, Lk + HL);
+    const int P = (hl == threadIdx.x) ? p0 : p1;
+    // row interchange 0 <-> P in every column
     const double v0 = A_(0);
     double n0 = v0;
 #pragma unroll
@@ -157,35 +174,49 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
         n0 = s ? A_(i) : n0;
         A_(i) = s ? v0 : A_(i);
     }
+    // multipliers of the pivot column, handed to the half through LDS (in order within
+    // the wavefront, so no barrier)
+    if (hl == Lk) {
+        sing = sing || !(best > 0.0);
+        const double rp = recip(n0);
 #pragma unroll
-    for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], n0, A_(i));
+        for (int i = 1; i < WR; ++i) slot[i] = A_(i) * rp;
+        U[k * UW] = rp;  // the diagonal of U is stored inverted: back substitution multiplies
+    }
+    __builtin_amdgcn_wave_barrier();
+    double l[WR];
+#pragma unroll
+    for (int i = 1; i < WR; ++i) l[i] = slot[i];
+    // rank-1 update; the pivot column leaves the window (column k+19, zero in rows
+    // k+1..k+9, takes its lane), so its rows are cleared instead
+    const double keep = (hl == Lk) ? 0.0 : 1.0;
+#pragma unroll
+    for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], n0, A_(i)) * keep;
     // U row k: lane column c -> offset c - k; right-hand sides at WC..WC+2
-    if (hl < WC)
-        U[k * UW + (hl >= Lk ? hl - Lk : hl - Lk + WC)] = n0;
-    else if (hl < UW)
+    if (hl < WC) {
+        if (hl != Lk) U[k * UW + (hl >= Lk ? hl - Lk : hl - Lk + WC)] = n0;
+    } else if (hl < UW)
         U[k * UW + hl] = n0;
     __builtin_amdgcn_wave_barrier();  // slot is rewritten by the next step
-    // slide: the pivot column leaves, column k+19 enters (zero in rows k+1..k+9);
-    // logical row 0's register becomes row k+10
-    if (hl == Lk) {
-        col += WC;
-        pc = decode<M>(col);
-#pragma unroll
-        for (int i = 1; i < WR; ++i) A_(i) = 0.0;
-    }
-    A_(0) = window_entry<M, HAS_ED>(hl, k + WR, pc, tp, q2, w, ed);
+    // slide: logical row 0's register becomes row k+10
+    if (hl == Lk) col += WC;
+    A_(0) = row_entry<M, HAS_ED>(hl, k + WR, col, desc, val, w, ed);
 #undef A_
 }
 
+#ifndef TGMS_BAND_LB
+#define TGMS_BAND_LB 1  // minimum wavefronts per SIMD the register allocation must allow
+#endif
+
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
+__global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
                                                   const int32_t* __restrict__ seg_offsets,
                                                   const double* __restrict__ W, const double* __restrict__ T,
                                                   const double* __restrict__ ED, double* __restrict__ C,
                                                   int32_t* __restrict__ status, double* __restrict__ scratch) {
     constexpr int N = 14 * M + 2;
-    __shared__ double s_tp[2][M * 8];       // T_i^e, e = 0..7
-    __shared__ double s_q2[2][M * 16];      // 2 Q_i, rows/cols 4..7 (a1)
+    __shared__ int s_desc[NDESC];           // entry pattern of the interleaved KKT
+    __shared__ double s_val[2][M * VAL];    // V_i = [1, T_i^0..T_i^7, 2Q_i] per segment
     __shared__ double s_w[2][(M + 1) * 3];  // waypoints
     __shared__ double s_ed[2][18];          // end derivatives (HAS_ED)
     __shared__ double s_slot[2][WR];        // pivot index + multipliers of the current step
@@ -193,8 +224,11 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
 
     const int lane = threadIdx.x, h = lane >> 5, hl = lane & (HL - 1);
     double* U = scratch + ((size_t)blockIdx.x * 2 + h) * (size_t)N * UW;
-    double* tp = s_tp[h];
-    double* q2 = s_q2[h];
+    double* val = s_val[h];
+    for (int q = lane; q < NDESC; q += W64) {
+        const int vv = q / (NOFF * WC), rem = q - vv * NOFF * WC, o = rem / WC - 4, d = rem % WC - KL;
+        s_desc[q] = desc_entry(vv, o, d);
+    }
     double* w = s_w[h];
     double* ed = s_ed[h];
     double* slot = s_slot[h];
@@ -224,11 +258,12 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
             const double t = gt[hl];
             ok = ok && finite_pos(t);
             double p = 1.0;
-            tp[hl * 8] = 1.0;
+            val[hl * VAL] = 1.0;
+            val[hl * VAL + 1] = 1.0;
 #pragma unroll
             for (int e = 1; e < 8; ++e) {
                 p *= t;
-                tp[hl * 8 + e] = p;
+                val[hl * VAL + 1 + e] = p;
             }
         }
         const unsigned long long badm = __ballot(!ok);
@@ -236,22 +271,21 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
         __builtin_amdgcn_wave_barrier();
         for (int q = hl; q < M * 16; q += HL) {
             const int i = q >> 4, j = 4 + ((q >> 2) & 3), kk = 4 + (q & 3), ex = j + kk - 7;
-            q2[q] = 2.0 * (dfac(j, 4) * dfac(kk, 4) * tp[i * 8 + ex] / (double)ex);
+            val[i * VAL + 9 + (q & 15)] = 2.0 * (dfac(j, 4) * dfac(kk, 4) * val[i * VAL + 1 + ex] / (double)ex);
         }
         __builtin_amdgcn_wave_barrier();
 
         // ---- forward elimination (a3): window rows 0..9, columns hl
         int col = hl;
-        Pos pc = decode<M>(hl < WC ? col : N);
         double a[WR];
 #pragma unroll
-        for (int i = 0; i < WR; ++i) a[i] = window_entry<M, HAS_ED>(hl, i, pc, tp, q2, w, ed);
+        for (int i = 0; i < WR; ++i) a[i] = row_entry<M, HAS_ED>(hl, i, col, s_desc, val, w, ed);
         bool sing = false;
         int Lk = 0;
         for (int k0 = 0; k0 < N; k0 += WR) {
 #define STEP(R)                                                                                         \
     if (k0 + R < N) {                                                                                   \
-        elim_step<M, HAS_ED, R>(k0 + R, Lk, hl, a, col, pc, sing, slot, U, tp, q2, w, ed);              \
+        elim_step<M, HAS_ED, R>(k0 + R, Lk, hl, a, col, sing, slot, U, s_desc, val, w, ed);              \
         Lk = (Lk == WC - 1) ? 0 : Lk + 1;                                                               \
     }
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
@@ -266,57 +300,54 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
         // the U rows this wave stored are read back by other lanes: complete the stores and
         // drop stale L1 lines (the slab is reused by the next trajectory pair)
         __threadfence();
-        double y0 = 0.0, y1 = 0.0, y2 = 0.0;
+        // Lane hl < WC holds y of its pending row r = hl (mod WC) in [k-18, k] and, loaded
+        // a full lap (19 steps) ahead, the eliminated right-hand side of its next row r-19.
+        // At step k it needs U[r][k-r]: those come through a PFB-deep ring of loads.
         const int kN = N - 1;
         int LkB = kN % WC;
+        double y0 = 0.0, y1 = 0.0, y2 = 0.0, yb0 = 0.0, yb1 = 0.0, yb2 = 0.0;
         if (hl < WC) {
-            const int d = (LkB >= hl) ? LkB - hl : LkB - hl + WC;  // row kN - d
-            if (kN - d >= 0) {
-                const double* ur = U + (size_t)(kN - d) * UW + WC;
+            const int d = (LkB >= hl) ? LkB - hl : LkB - hl + WC;
+            const int r = kN - d;
+            if (r >= 0) {
+                const double* ur = U + (size_t)r * UW + WC;
                 y0 = ur[0];
                 y1 = ur[1];
                 y2 = ur[2];
             }
+            if (r - WC >= 0) {
+                const double* ur = U + (size_t)(r - WC) * UW + WC;
+                yb0 = ur[0];
+                yb1 = ur[1];
+                yb2 = ur[2];
+            }
         }
-        // prefetch ring: ud = U[k-d][d] for this lane, yn = y of the row k-19 (Lk lane)
-        double ud[PF], yn[PF][3];
+        double ud[PFB];
         auto issue = [&](int k, int slotk, int lk) {
-            ud[slotk] = 0.0;
-            yn[slotk][0] = yn[slotk][1] = yn[slotk][2] = 0.0;
-            if (k >= 0 && hl < WC) {
-                const int d = (lk >= hl) ? lk - hl : lk - hl + WC;
-                if (k - d >= 0) ud[slotk] = U[(size_t)(k - d) * UW + d];
-                if (d == 0 && k - WC >= 0) {
-                    const double* ur = U + (size_t)(k - WC) * UW + WC;
-                    yn[slotk][0] = ur[0];
-                    yn[slotk][1] = ur[1];
-                    yn[slotk][2] = ur[2];
-                }
-            }
+            const int d = (lk >= hl) ? lk - hl : lk - hl + WC;
+            ud[slotk] = (k >= 0 && hl < WC && k - d >= 0) ? U[(size_t)(k - d) * UW + d] : 0.0;
         };
-        {
-            int lk = LkB;
+        int lkPF = LkB;
 #pragma unroll
-            for (int s = 0; s < PF; ++s) {
-                issue(kN - s, s, lk);
-                lk = (lk == 0) ? WC - 1 : lk - 1;
-            }
+        for (int s = 0; s < PFB; ++s) {
+            issue(kN - s, s, lkPF);
+            lkPF = (lkPF == 0) ? WC - 1 : lkPF - 1;
         }
         double* xs = s_x[h];
         double* out = C + s0 * 24;
         double fin = 0.0;
-        int lkPF = LkB;  // pivot lane of step k - PF, kept for issue()
+#ifdef TGMS_BAND_NOBACK  // diagnostic: forward elimination only
+        for (int k0 = -1; k0 >= 0; k0 -= PFB) {
+#else
+        for (int k0 = kN; k0 >= 0; k0 -= PFB) {
+#endif
 #pragma unroll
-        for (int s = 0; s < PF; ++s) lkPF = (lkPF == 0) ? WC - 1 : lkPF - 1;
-        for (int k0 = kN; k0 >= 0; k0 -= PF) {
-#pragma unroll
-            for (int s = 0; s < PF; ++s) {
+            for (int s = 0; s < PFB; ++s) {
                 const int k = k0 - s;
                 if (k >= 0) {
                     const double u = ud[s];
-                    if (hl == LkB) {
-                        const double rd = 1.0 / u;  // u = U[k][0], the pivot
-                        const double x0 = y0 * rd, x1 = y1 * rd, x2 = y2 * rd;
+                    if (hl == LkB) {  // u = 1 / U[k][k]
+                        const double x0 = y0 * u, x1 = y1 * u, x2 = y2 * u;
                         xs[0] = x0;
                         xs[1] = x1;
                         xs[2] = x2;
@@ -328,9 +359,16 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
                             o[8] = emit ? x1 : 0.0;
                             o[16] = emit ? x2 : 0.0;
                         }
-                        y0 = yn[s][0];
-                        y1 = yn[s][1];
-                        y2 = yn[s][2];
+                        // take row k-19 (its right-hand side arrived a lap ago), fetch the next
+                        y0 = yb0;
+                        y1 = yb1;
+                        y2 = yb2;
+                        if (k - 2 * WC >= 0) {
+                            const double* ur = U + (size_t)(k - 2 * WC) * UW + WC;
+                            yb0 = ur[0];
+                            yb1 = ur[1];
+                            yb2 = ur[2];
+                        }
                     }
                     __builtin_amdgcn_wave_barrier();
                     const double x0 = xs[0], x1 = xs[1], x2 = xs[2];
@@ -340,13 +378,12 @@ __global__ __launch_bounds__(W64) void k_band_kkt(int32_t n_traj, const int32_t*
                         y2 = fma(-u, x2, y2);
                     }
                     __builtin_amdgcn_wave_barrier();
-                    issue(k - PF, s, lkPF);
+                    issue(k - PFB, s, lkPF);
                     LkB = (LkB == 0) ? WC - 1 : LkB - 1;
                     lkPF = (lkPF == 0) ? WC - 1 : lkPF - 1;
                 }
             }
         }
-        // status; non-finite solution check over the written coefficients
         const unsigned long long nf = __ballot(!(fin == 0.0));
         const bool nonfinite = ((h ? (nf >> 32) : nf) & 0xffffffffull) != 0;
         if (live && hl == 0 && status) {
@@ -365,7 +402,17 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
                   const double* ED, double* C, int32_t* status, double* scratch, int32_t grid,
                   hipStream_t stream) {
     if (n_traj <= 0) return hipSuccess;
-    const int32_t g = std::min<int32_t>(grid, (n_traj + 1) / 2);
+    // persistent grid: only as many wavefronts as are resident at once (a second,
+    // partial round of wavefronts would double the tail)
+    static int occ[2] = {0, 0};
+    int& nb = occ[ED ? 1 : 0];
+    if (nb == 0) {
+        hipError_t e = ED ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, true>, W64, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, false>, W64, 0);
+        if (e != hipSuccess || nb <= 0) nb = BAND_WAVES_PER_CU;
+    }
+    const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, BAND_WAVES_PER_CU);
+    const int32_t g = std::min<int32_t>(std::min(grid, resident), (n_traj + 1) / 2);
     if (ED)
         hipLaunchKernelGGL((k_band_kkt<M, true>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
                            status, scratch);

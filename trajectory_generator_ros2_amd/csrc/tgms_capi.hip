@@ -236,17 +236,13 @@ tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, 
     return run_parallel(h, stream, jobs);
 }
 
-#ifndef TGMS_BAND_WAVES_PER_CU
-#define TGMS_BAND_WAVES_PER_CU 16
-#endif
-
 // Band-KKT scratch for largest M `m_max`; the slabs are per wavefront of one launch,
 // so launches sharing them are serialised on one stream.
 tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream) {
     if (h->band_grid == 0) {
         int cus = 0;
         TGMS_HIP(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-        h->band_grid = std::max(1, cus) * TGMS_BAND_WAVES_PER_CU;
+        h->band_grid = std::max(1, cus) * tgms::BAND_WAVES_PER_CU;
     }
     const size_t need = tgms::band_scratch_bytes(m_max, h->band_grid);
     if (need <= h->band_cap) return TGMS_OK;
