@@ -72,7 +72,9 @@ typedef enum tgms_method {
     TGMS_METHOD_BAND_KKT = 2   /* the same KKT and LU with partial pivoting, in the
                                  segment-interleaved order where it is banded (kl = ku = 9);
                                  the structurally-zero entries are skipped, half a wavefront
-                                 per trajectory, M <= TGMS_MAX_SEGMENTS */
+                                 per trajectory, M <= TGMS_MAX_SEGMENTS.  Its U rows live in a
+                                 handle-owned scratch slab: solves of one handle on different
+                                 streams must not overlap in time */
 } tgms_method;
 
 typedef enum tgms_yaw_mode {

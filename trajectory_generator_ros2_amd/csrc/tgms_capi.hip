@@ -206,6 +206,33 @@ tgms_status run_parallel(tgms_handle* h, hipStream_t stream,
     return TGMS_OK;
 }
 
+// Independent chains of dependent launches: chain j runs in order on its own stream
+// (forked from `stream`, joined back), and the launches are issued round-robin across
+// the chains.
+tgms_status run_chains(tgms_handle* h, hipStream_t stream,
+                       const std::vector<std::vector<std::function<hipError_t(hipStream_t)>>>& chains) {
+    if (chains.size() <= 1 || (int)chains.size() > TGMS_AUX_STREAMS) {
+        for (auto& ch : chains)
+            for (auto& op : ch) TGMS_HIP(h, op(stream));
+        return TGMS_OK;
+    }
+    tgms_status s = ensure_aux(h);
+    if (s != TGMS_OK) return s;
+    const int used = (int)chains.size();
+    TGMS_HIP(h, hipEventRecord(h->fork_ev, stream));
+    for (int j = 0; j < used; ++j) TGMS_HIP(h, hipStreamWaitEvent(h->aux[j], h->fork_ev, 0));
+    size_t longest = 0;
+    for (auto& ch : chains) longest = std::max(longest, ch.size());
+    for (size_t i = 0; i < longest; ++i)
+        for (int j = 0; j < used; ++j)
+            if (i < chains[j].size()) TGMS_HIP(h, chains[j][i](h->aux[j]));
+    for (int j = 0; j < used; ++j) {
+        TGMS_HIP(h, hipEventRecord(h->join_ev[j], h->aux[j]));
+        TGMS_HIP(h, hipStreamWaitEvent(stream, h->join_ev[j], 0));
+    }
+    return TGMS_OK;
+}
+
 // Reduced method, ragged plan: every M group in one launch per occupancy class
 // (M <= 11 / M >= 12), the longest groups' wavefronts first.
 void class_tables(const tgms_handle* h, const Plan& p, tgms::GroupTable (&tab)[2]) {
@@ -321,27 +348,33 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         // the GPU).
         tgms::GroupTable tab[2];
         class_tables(h, p, tab);
-        std::vector<std::function<hipError_t(hipStream_t)>> jobs;
-        for (int k = 1; k >= 0; --k)
-            if (tab[k].ngroups)
-                jobs.push_back([&, k](hipStream_t q) -> hipError_t {
-                    int c = 0;
-                    for (int32_t it = 0; it < iters; ++it, c ^= 1) {
-                        const hipError_t e = tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, eta,
-                                                                       T[c ^ 1], nullptr, nullptr, st, q);
-                        if (e != hipSuccess) return e;
-                    }
-                    if (cost) {
-                        const hipError_t e = tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, 0.0,
-                                                                       T[c ^ 1], cost, nullptr, st, q);
-                        if (e != hipSuccess) return e;
-                    }
-                    if (C)
-                        return tgms::launch_ragged_multi(k, tab[k], false, d_so, W, T[c], ED, 0.0, 0.0, nullptr,
-                                                         nullptr, C, st, q);
-                    return hipSuccess;
+        // one op list per class; ops are issued round-robin across the classes so a
+        // captured graph holds them interleaved and launches both chains side by side
+        // (capturing one whole chain first held the other back by its ~80 us of
+        // submissions)
+        std::vector<std::vector<std::function<hipError_t(hipStream_t)>>> chains;
+        for (int k = 1; k >= 0; --k) {
+            if (!tab[k].ngroups) continue;
+            std::vector<std::function<hipError_t(hipStream_t)>> ops;
+            int c = 0;
+            for (int32_t it = 0; it < iters; ++it, c ^= 1)
+                ops.push_back([&, k, c](hipStream_t q) {
+                    return tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, eta, T[c ^ 1], nullptr,
+                                                     nullptr, st, q);
                 });
-        tgms_status s = run_parallel(h, stream, jobs);
+            if (cost)
+                ops.push_back([&, k, c](hipStream_t q) {
+                    return tgms::launch_ragged_multi(k, tab[k], true, d_so, W, T[c], ED, kT, 0.0, T[c ^ 1], cost,
+                                                     nullptr, st, q);
+                });
+            if (C)
+                ops.push_back([&, k, c](hipStream_t q) {
+                    return tgms::launch_ragged_multi(k, tab[k], false, d_so, W, T[c], ED, 0.0, 0.0, nullptr, nullptr,
+                                                     C, st, q);
+                });
+            chains.push_back(std::move(ops));
+        }
+        tgms_status s = run_chains(h, stream, chains);
         if (s != TGMS_OK) return s;
         *cur = iters & 1;
         return TGMS_OK;
