@@ -1,0 +1,106 @@
+"""GPU edge cases of the solve, for every method: empty and single-trajectory batches,
+stationary goals (all waypoints equal), the largest M at swarm scale, and a ragged
+batch whose groups include one-trajectory groups.  Tolerance as everywhere: norm-wise
+per (trajectory, axis) <= 1e-9 against the oracle."""
+import numpy as np
+import pytest
+
+from conftest import batch_rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+
+
+def _methods():
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
+    return [METHOD_REDUCED, METHOD_DENSE_KKT, METHOD_BAND_KKT]
+
+
+@pytest.fixture(params=[0, 1, 2], ids=["reduced", "dense", "band"])
+def method(request, solver):
+    solver.set_method(_methods()[request.param])
+    yield request.param
+    solver.set_method(_methods()[0])
+
+
+def test_empty_batch(solver, method):
+    import torch
+    C, st, worst = solver.solve(np.zeros(1, np.int32), np.zeros((0, 3)), np.zeros(0))
+    assert worst == 0 and C.shape == (0, 3, 8) and st.shape == (0,)
+    e = torch.empty((0,), dtype=torch.float64, device="cuda")
+    solver.solve_uniform_device(0, 3, e, e, e, None)  # no launch, no error
+
+
+@pytest.mark.parametrize("M", [1, 3, 10])
+def test_single_trajectory(solver, oracle, method, M):
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(1, M, seed=5000 + M)
+    C, st, worst = solver.solve(so, W.reshape(-1, 3), T.reshape(-1))
+    assert worst == 0 and st[0] == 0
+    R, _ = oracle.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, oracle.KKT_C4)
+    assert batch_rel_err(so, C, R) <= TOL
+
+
+def test_stationary_goal(solver, method):
+    """All waypoints equal, rest to rest: the optimum is the constant polynomial, so every
+    coefficient but c0 is exactly 0 and c0 is the waypoint."""
+    B, M = 40, 6
+    so = np.arange(B + 1, dtype=np.int32) * M
+    W = np.repeat(np.random.default_rng(1).uniform(-5, 5, size=(B, 1, 3)), M + 1, axis=1).reshape(-1, 3)
+    T = np.random.default_rng(2).uniform(0.5, 3.0, size=B * M)
+    C, st, worst = solver.solve(so, W, T)
+    assert worst == 0
+    C = C.reshape(B, M, 3, 8)
+    assert np.abs(C[..., 1:]).max() <= 1e-9
+    w0 = W.reshape(B, M + 1, 3)[:, :1, :]
+    assert np.abs(C[..., 0] - w0).max() <= 1e-9 * np.abs(w0).max()
+
+
+def test_ragged_single_member_groups(solver, oracle, method):
+    """Every M group holds one trajectory (one partially filled wavefront per group)."""
+    from trajectory_generator_ros2_amd import synthetic as S
+    hi = 10 if method == 1 else 16
+    Ms = np.arange(1, hi + 1)
+    so = np.concatenate([[0], np.cumsum(Ms)]).astype(np.int32)
+    rng = np.random.default_rng(6000)
+    W = np.concatenate([S.uniform_batch(1, int(m), seed=6000 + int(m))[1].reshape(-1, 3) for m in Ms])
+    T = np.concatenate([S.uniform_batch(1, int(m), seed=6000 + int(m))[2].reshape(-1) for m in Ms])
+    perm = rng.permutation(len(Ms))  # groups not in M order in the batch
+    so_p = np.concatenate([[0], np.cumsum(Ms[perm])]).astype(np.int32)
+    W_p = np.concatenate([W[so[b] + b: so[b + 1] + b + 1] for b in perm])
+    T_p = np.concatenate([T[so[b]: so[b + 1]] for b in perm])
+    C, st, worst = solver.solve(so_p, W_p, T_p)
+    assert worst == 0 and (st == 0).all()
+    R, _ = oracle.solve_batch(so_p, W_p, T_p, None, oracle.REDUCED)
+    assert batch_rel_err(so_p, C, R) <= TOL
+
+
+def test_largest_m_at_swarm_scale(solver, oracle):
+    """M = 16 (the largest supported) for 131,072 trajectories (config-4 shard size, 403 MB
+    of coefficients) through the device API, reduced and band methods: the first and last
+    256 trajectories against the oracle, every status OK, the two methods agree on all."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    B, M = 131072, 16
+    so, W, T = S.uniform_batch(B, M, seed=7000)
+    dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+    out = {}
+    for meth in (METHOD_REDUCED, METHOD_BAND_KKT):
+        solver.set_method(meth)
+        dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+        dS = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS)
+        torch.cuda.synchronize()
+        assert int((dS != 0).sum()) == 0
+        out[meth] = dC
+    solver.set_method(METHOD_REDUCED)
+    err = (out[METHOD_BAND_KKT] - out[METHOD_REDUCED]).abs().amax(dim=(1, 3)) / \
+        out[METHOD_REDUCED].abs().amax(dim=(1, 3))
+    assert float(err.max()) <= TOL
+    for sl in (slice(0, 256), slice(B - 256, B)):
+        sub_so = (np.arange(257, dtype=np.int32) * M)
+        R, _ = oracle.solve_batch(sub_so, W[sl].reshape(-1, 3), T[sl].reshape(-1), None, oracle.REDUCED)
+        C = out[METHOD_BAND_KKT][sl].reshape(-1, 3, 8).cpu().numpy()
+        assert batch_rel_err(sub_so, C, R) <= TOL
