@@ -154,18 +154,19 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
                                           const double* w, const double* ed) {
 #define A_(i) a[(R0 + (i)) % WR]
     // pivot search in every lane's own column; the pivot column's lane Lk decides
-    double best = fabs(A_(0));
+    double bv = A_(0);
     int p = 0;
 #pragma unroll
     for (int i = 1; i < WR; ++i) {
-        const double v = fabs(A_(i));
-        p = (v > best) ? i : p;
-        best = fmax(best, v);
+        const bool g = fabs(A_(i)) > fabs(bv);
+        bv = g ? A_(i) : bv;
+        p = g ? i : p;
     }
     // the two halves' pivot rows (lanes Lk and Lk + 32) through the scalar unit
     const int p0 = __builtin_amdgcn_readlane(p, Lk), p1 = __builtin_amdgcn_readlane(p, Lk + HL);
+    // row interchange 0 <-> P in every column (selects: a branch per pivot row makes the
+    // register allocator copy the whole window at every join)
     const int P = (hl == threadIdx.x) ? p0 : p1;
-    // row interchange 0 <-> P in every column
     const double v0 = A_(0);
     double n0 = v0;
 #pragma unroll
@@ -174,6 +175,7 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
         n0 = s ? A_(i) : n0;
         A_(i) = s ? v0 : A_(i);
     }
+    const double best = fabs(bv);
     // multipliers of the pivot column, handed to the half through LDS (in order within
     // the wavefront, so no barrier)
     if (hl == Lk) {
