@@ -140,6 +140,11 @@ __device__ __forceinline__ double row_entry(int hl, int r, int c, const int* des
     return (double)(de >> 5) * val[i * VAL + (de & 31)];
 }
 
+// U-slab load that misses L1 (an agent-scope relaxed atomic load: sc1)
+__device__ __forceinline__ double ld_u(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // 1/x: hardware reciprocal + two Newton steps (within an ulp; the pivots only scale)
 __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
@@ -178,22 +183,27 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
     const double best = fabs(bv);
     // multipliers of the pivot column, handed to the half through LDS (in order within
     // the wavefront, so no barrier)
+    // The pivot column leaves the window (its lane takes column k+19, zero in rows
+    // k+1..k+9): its rows are cleared here and its update below multiplies by 0.
+    double nu = n0;
     if (hl == Lk) {
         sing = sing || !(best > 0.0);
         const double rp = recip(n0);
 #pragma unroll
-        for (int i = 1; i < WR; ++i) slot[i] = A_(i) * rp;
+        for (int i = 1; i < WR; ++i) {
+            slot[i] = A_(i) * rp;
+            A_(i) = 0.0;
+        }
+        nu = 0.0;
         U[k * UW] = rp;  // the diagonal of U is stored inverted: back substitution multiplies
     }
     __builtin_amdgcn_wave_barrier();
     double l[WR];
 #pragma unroll
     for (int i = 1; i < WR; ++i) l[i] = slot[i];
-    // rank-1 update; the pivot column leaves the window (column k+19, zero in rows
-    // k+1..k+9, takes its lane), so its rows are cleared instead
-    const double keep = (hl == Lk) ? 0.0 : 1.0;
+    // rank-1 update
 #pragma unroll
-    for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], n0, A_(i)) * keep;
+    for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], nu, A_(i));
     // U row k: lane column c -> offset c - k; right-hand sides at WC..WC+2
     if (hl < WC) {
         if (hl != Lk) U[k * UW + (hl >= Lk ? hl - Lk : hl - Lk + WC)] = n0;
@@ -299,9 +309,12 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
 
         // ---- back substitution, column oriented: lane hl < WC holds y for the pending
         // row r = hl (mod WC) in [k-18, k]; at step k that row needs U[r][k-r].
-        // the U rows this wave stored are read back by other lanes: complete the stores and
-        // drop stale L1 lines (the slab is reused by the next trajectory pair)
-        __threadfence();
+        // The U rows this wave stored are read back by other lanes of the wave: wait for
+        // the stores to reach L2, and read them with L1-bypassing loads (ld_u: the slab is
+        // reused by the next pair, so L1 may hold the previous pair's lines).  An
+        // agent-scope fence here instead (buffer_wbl2: write back the XCD's L2) cost the
+        // whole kernel.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // Lane hl < WC holds y of its pending row r = hl (mod WC) in [k-18, k] and, loaded
         // a full lap (19 steps) ahead, the eliminated right-hand side of its next row r-19.
         // At step k it needs U[r][k-r]: those come through a PFB-deep ring of loads.
@@ -313,21 +326,21 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
             const int r = kN - d;
             if (r >= 0) {
                 const double* ur = U + (size_t)r * UW + WC;
-                y0 = ur[0];
-                y1 = ur[1];
-                y2 = ur[2];
+                y0 = ld_u(ur);
+                y1 = ld_u(ur + 1);
+                y2 = ld_u(ur + 2);
             }
             if (r - WC >= 0) {
                 const double* ur = U + (size_t)(r - WC) * UW + WC;
-                yb0 = ur[0];
-                yb1 = ur[1];
-                yb2 = ur[2];
+                yb0 = ld_u(ur);
+                yb1 = ld_u(ur + 1);
+                yb2 = ld_u(ur + 2);
             }
         }
         double ud[PFB];
         auto issue = [&](int k, int slotk, int lk) {
             const int d = (lk >= hl) ? lk - hl : lk - hl + WC;
-            ud[slotk] = (k >= 0 && hl < WC && k - d >= 0) ? U[(size_t)(k - d) * UW + d] : 0.0;
+            ud[slotk] = (k >= 0 && hl < WC && k - d >= 0) ? ld_u(U + (size_t)(k - d) * UW + d) : 0.0;
         };
         int lkPF = LkB;
 #pragma unroll
@@ -367,9 +380,9 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
                         y2 = yb2;
                         if (k - 2 * WC >= 0) {
                             const double* ur = U + (size_t)(k - 2 * WC) * UW + WC;
-                            yb0 = ur[0];
-                            yb1 = ur[1];
-                            yb2 = ur[2];
+                            yb0 = ld_u(ur);
+                            yb1 = ld_u(ur + 1);
+                            yb2 = ld_u(ur + 2);
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
