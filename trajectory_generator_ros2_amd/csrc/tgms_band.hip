@@ -195,7 +195,10 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
             A_(i) = 0.0;
         }
         nu = 0.0;
-        U[k * UW] = rp;  // the diagonal of U is stored inverted: back substitution multiplies
+#ifndef TGMS_BAND_NOUSTORE
+        U[k * UW] = rp;
+#endif
+        (void)0;  // the diagonal of U is stored inverted: back substitution multiplies
     }
     __builtin_amdgcn_wave_barrier();
     double l[WR];
@@ -205,7 +208,11 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
 #pragma unroll
     for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], nu, A_(i));
     // U row k: lane column c -> offset c - k; right-hand sides at WC..WC+2
+#ifdef TGMS_BAND_NOUSTORE  // diagnostic: no U stores (wrong results)
+    if (k < 0) {
+#else
     if (hl < WC) {
+#endif
         if (hl != Lk) U[k * UW + (hl >= Lk ? hl - Lk : hl - Lk + WC)] = n0;
     } else if (hl < UW)
         U[k * UW + hl] = n0;
