@@ -33,8 +33,23 @@ namespace {
 constexpr int KL = 9;              // sub-diagonals (== super-diagonals) of the interleaved KKT
 constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
-constexpr int UW = WC + 3;         // scratch row: U row + 3 eliminated right-hand sides
+constexpr int UW = 32;             // scratch row: U row (19) + 3 eliminated right-hand sides, padded
+                                   // to one lane per entry of the half (stores need no lane mask)
 constexpr int HL = 32;             // lanes per trajectory
+#ifdef TGMS_BAND_STAMPS  // diagnostic build: s_memtime at phase boundaries, lane 0 of blocks < 64, first pair
+constexpr int BST_BLOCKS = 64, BST_STEPS = 160, BST_PH = 8;
+__device__ unsigned long long g_bstamps[BST_BLOCKS * BST_STEPS * BST_PH];
+#define BSTAMP(k, i)                                                                                    \
+    do {                                                                                                \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                     \
+        if (blockIdx.x < BST_BLOCKS && threadIdx.x == 0 && (k) < BST_STEPS && first_pair)              \
+            g_bstamps[(blockIdx.x * BST_STEPS + (k)) * BST_PH + (i)] = __builtin_amdgcn_s_memtime();     \
+    } while (0)
+#else
+#define BSTAMP(k, i) \
+    do {             \
+    } while (0)
+#endif
 constexpr int PFB = 16;            // back-substitution prefetch depth (steps)
 
 // Position q of the interleaved order.  kind: 0 start row (idx = derivative k),
@@ -117,27 +132,40 @@ __device__ int desc_entry(int vv, int o, int d) {
 }
 
 // Row r (wave-uniform) at this lane's column c; lanes WC..WC+2 return the right-hand
-// side b_r of axis hl - WC.
+// side b_r of axis hl - WC.  Branch-free in the lane: every lane reads its matrix entry
+// and the right-hand-side candidate and selects (a divergent split costs more issue
+// slots than the two extra LDS reads).
 template <int M, bool HAS_ED>
 __device__ __forceinline__ double row_entry(int hl, int r, int c, const int* desc, const double* val,
                                             const double* w, const double* ed) {
     constexpr int N = 14 * M + 2;
-    if (r >= N || hl >= UW) return 0.0;
+    if (r >= N) return 0.0;
     const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
     const int o = r - (4 + 14 * i);
-    if (hl >= WC) {  // right-hand sides
-        const int a = hl - WC;
-        if (o < 0) return o == -4 ? w[a] : (HAS_ED ? ed[(o + 3) * 3 + a] : 0.0);
-        if (o < 8) return 0.0;
+    // right-hand-side source (uniform): waypoint row wr or end-derivative base eb
+    int wr = -1, eb = -1;
+    if (o < 0) {
+        if (o == -4) wr = 0;
+        else eb = (o + 3) * 3;
+    } else if (o >= 8) {
         const int t = o - 8;
-        if (i == M - 1) return t == 0 ? w[M * 3 + a] : (HAS_ED ? ed[9 + (t - 1) * 3 + a] : 0.0);
-        return t <= 1 ? w[(i + 1) * 3 + a] : 0.0;
+        if (i == M - 1) {
+            if (t == 0) wr = M;
+            else eb = 9 + (t - 1) * 3;
+        } else if (t <= 1) {
+            wr = i + 1;
+        }
     }
+    const int ax = min(max(hl - WC, 0), 2);
+    const double rw = w[max(wr, 0) * 3 + ax];
+    const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
+    const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
     const int d = c - r;
-    if (c >= N || d < -KL || d > KL) return 0.0;
+    const bool inb = (c < N) && d >= -KL && d <= KL;
     const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
-    const int de = desc[(vv * NOFF + o + 4) * WC + d + KL];
-    return (double)(de >> 5) * val[i * VAL + (de & 31)];
+    const int de = desc[(vv * NOFF + o + 4) * WC + min(max(d, -KL), KL) + KL];
+    const double m = (double)(de >> 5) * val[i * VAL + (de & 31)];
+    return (hl < WC) ? (inb ? m : 0.0) : ((hl < WC + 3) ? rhs : 0.0);
 }
 
 // U-slab load that misses L1 (an agent-scope relaxed atomic load: sc1)
@@ -156,8 +184,9 @@ __device__ __forceinline__ double recip(double x) {
 template <int M, bool HAS_ED, int R0>
 __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR], int& col, bool& sing,
                                           double* slot, double* U, const int* desc, const double* val,
-                                          const double* w, const double* ed) {
+                                          const double* w, const double* ed, bool first_pair) {
 #define A_(i) a[(R0 + (i)) % WR]
+    BSTAMP(k, 0);
     // pivot search in every lane's own column; the pivot column's lane Lk decides
     double bv = A_(0);
     int p = 0;
@@ -167,6 +196,7 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
         bv = g ? A_(i) : bv;
         p = g ? i : p;
     }
+    BSTAMP(k, 1);
     // the two halves' pivot rows (lanes Lk and Lk + 32) through the scalar unit
     const int p0 = __builtin_amdgcn_readlane(p, Lk), p1 = __builtin_amdgcn_readlane(p, Lk + HL);
     // row interchange 0 <-> P in every column (selects: a branch per pivot row makes the
@@ -181,25 +211,23 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
         A_(i) = s ? v0 : A_(i);
     }
     const double best = fabs(bv);
+    BSTAMP(k, 2);
     // multipliers of the pivot column, handed to the half through LDS (in order within
     // the wavefront, so no barrier)
     // The pivot column leaves the window (its lane takes column k+19, zero in rows
     // k+1..k+9): its rows are cleared here and its update below multiplies by 0.
     double nu = n0;
+    const double rp = recip(n0);
     if (hl == Lk) {
         sing = sing || !(best > 0.0);
-        const double rp = recip(n0);
 #pragma unroll
         for (int i = 1; i < WR; ++i) {
             slot[i] = A_(i) * rp;
             A_(i) = 0.0;
         }
         nu = 0.0;
-#ifndef TGMS_BAND_NOUSTORE
-        U[k * UW] = rp;
-#endif
-        (void)0;  // the diagonal of U is stored inverted: back substitution multiplies
     }
+    BSTAMP(k, 3);
     __builtin_amdgcn_wave_barrier();
     double l[WR];
 #pragma unroll
@@ -207,19 +235,15 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
     // rank-1 update
 #pragma unroll
     for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], nu, A_(i));
-    // U row k: lane column c -> offset c - k; right-hand sides at WC..WC+2
-#ifdef TGMS_BAND_NOUSTORE  // diagnostic: no U stores (wrong results)
-    if (k < 0) {
-#else
-    if (hl < WC) {
-#endif
-        if (hl != Lk) U[k * UW + (hl >= Lk ? hl - Lk : hl - Lk + WC)] = n0;
-    } else if (hl < UW)
-        U[k * UW + hl] = n0;
+    BSTAMP(k, 4);
+    // U row k: lane column c -> offset c - k (the diagonal stored inverted: back
+    // substitution multiplies), right-hand sides at WC..WC+2, lanes beyond into padding
+    U[k * UW + (hl < WC ? (hl >= Lk ? hl - Lk : hl - Lk + WC) : hl)] = (hl == Lk) ? rp : n0;
     __builtin_amdgcn_wave_barrier();  // slot is rewritten by the next step
     // slide: logical row 0's register becomes row k+10
     if (hl == Lk) col += WC;
     A_(0) = row_entry<M, HAS_ED>(hl, k + WR, col, desc, val, w, ed);
+    BSTAMP(k, 6);
 #undef A_
 }
 
@@ -254,6 +278,8 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
     const int npairs = (n_traj + 1) >> 1;
 
     for (int pr = blockIdx.x; pr < npairs; pr += gridDim.x) {
+        const bool first_pair = pr == (int)blockIdx.x;
+        (void)first_pair;
         const int bi = 2 * pr + h;
         const bool live = bi < n_traj;
         const int32_t b = ids ? ids[live ? bi : 2 * pr] : (live ? bi : 2 * pr);
@@ -304,7 +330,7 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
         for (int k0 = 0; k0 < N; k0 += WR) {
 #define STEP(R)                                                                                         \
     if (k0 + R < N) {                                                                                   \
-        elim_step<M, HAS_ED, R>(k0 + R, Lk, hl, a, col, sing, slot, U, s_desc, val, w, ed);              \
+        elim_step<M, HAS_ED, R>(k0 + R, Lk, hl, a, col, sing, slot, U, s_desc, val, w, ed, first_pair);              \
         Lk = (Lk == WC - 1) ? 0 : Lk + 1;                                                               \
     }
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
@@ -463,3 +489,9 @@ hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* ids, const int3
 }
 
 }  // namespace tgms
+
+#ifdef TGMS_BAND_STAMPS
+extern "C" int tgms_debug_band_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tgms::g_bstamps), sizeof(unsigned long long) * (size_t)n) == hipSuccess;
+}
+#endif
