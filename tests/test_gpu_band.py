@@ -118,3 +118,35 @@ def test_band_config3_device_matches_reduced(band):
     assert int((dS != 0).sum()) == 0
     err = (dC - dR).abs().amax(dim=(1, 3)) / dR.abs().amax(dim=(1, 3))
     assert float(err.max()) <= TOL
+
+
+def test_band_ragged_end_derivs_and_invalid(band, oracle):
+    """A ragged batch (every M in 1..16, groups solved one after another through the
+    shared U slabs) with end derivatives and invalid trajectories in several groups:
+    valid ones match the oracle, invalid ones are flagged and zeroed."""
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG
+    from trajectory_generator_ros2_amd import synthetic as S
+    rng = np.random.default_rng(913)
+    so, W, T = S.ragged_batch(600, 1, 16, seed=913)
+    B = len(so) - 1
+    ED = rng.normal(size=(B, 18))
+    T = T.copy()
+    M = np.diff(so)
+    bad = [int(np.flatnonzero(M == m)[0]) for m in (1, 6, 11, 16)]
+    for b in bad:
+        T[so[b]] = 0.0
+    C, st, worst = band.solve(so, W, T, ED)
+    assert worst == ERR_INVALID_ARG
+    assert all(st[b] == ERR_INVALID_ARG for b in bad)
+    good = np.setdiff1d(np.arange(B), bad)
+    assert (st[good] == 0).all()
+    for b in bad:
+        assert not C[so[b]:so[b + 1]].any()
+    T2 = T.copy()
+    for b in bad:
+        T2[so[b]] = 1.0
+    R, _ = oracle.solve_batch(so, W, T2, ED, oracle.KKT_BAND)
+    for b in good:
+        c, r = C[so[b]:so[b + 1]], R[so[b]:so[b + 1]]
+        for a in range(3):
+            assert np.abs(c[:, a] - r[:, a]).max() <= TOL * max(np.abs(r[:, a]).max(), 1e-300)
