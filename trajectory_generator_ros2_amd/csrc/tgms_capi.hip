@@ -341,6 +341,26 @@ tgms_status dispatch_refine(tgms_handle* h, const Plan& p, int32_t B, const int3
 tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_so, const double* W,
                         double* const T[2], const double* ED, double kT, double eta, int32_t iters, double* C,
                         double* cost, int32_t* st, hipStream_t stream, int* cur) {
+    static const bool stepwise = std::getenv("TGMS_REFINE_STEPWISE") != nullptr;
+    if (B > 0 && p.uniform_m == 0 && !stepwise) {
+        // Ragged: every step of a trajectory only involves that trajectory, so each
+        // occupancy class runs its whole loop (steps, cost, final solve) in ONE launch,
+        // times kept in LDS between steps and updated in place in T[0]; the two classes'
+        // launches run side by side.
+        tgms::GroupTable tab[2];
+        class_tables(h, p, tab);
+        std::vector<std::function<hipError_t(hipStream_t)>> jobs;
+        for (int k = 1; k >= 0; --k)
+            if (tab[k].ngroups)
+                jobs.push_back([&, k](hipStream_t q) {
+                    return tgms::launch_refine_loop_multi(k, tab[k], d_so, W, T[0], ED, kT, eta, iters, cost, C, st,
+                                                          q);
+                });
+        tgms_status s = run_parallel(h, stream, jobs);
+        if (s != TGMS_OK) return s;
+        *cur = 0;
+        return TGMS_OK;
+    }
     if (B > 0 && p.uniform_m == 0) {
         // Ragged: the two occupancy classes hold disjoint trajectories, so each runs its
         // whole chain (steps, cost, final solve) on its own stream and they meet once at

@@ -67,6 +67,13 @@ hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, cons
                                const double* W, const double* T, const double* ED, double kT, double eta,
                                double* Tout, double* cost, double* C, int32_t* status, hipStream_t stream);
 
+// The whole refinement loop of a ragged batch per occupancy class in one launch: iters
+// steps, the cost at the final times (cost nullable), the final solve into C (nullable);
+// T holds the initial times and receives the final ones (in place).
+hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* seg_offsets, const double* W,
+                                    double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
+                                    double* C, int32_t* status, hipStream_t stream);
+
 // Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,
                          const double* ED, const double* C, double dt, int yaw_mode,

@@ -2274,6 +2274,109 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
     if (live && !right && status) status[b] = st;
 }
 
+// The whole refinement loop of one wavefront's trajectories (config 5) in one pass:
+// `iters` steps, the cost at the final times, the final solve into C.  Trajectories
+// are independent across steps, so nothing synchronises beyond the wavefront: the times
+// stay in the LDS stage between steps (and in the lanes that own them), and T is read
+// once and written once (in place).  Step for step the same arithmetic as
+// refine_ragged_block + refine_update + reduced_ragged_block.
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int32_t n,
+                                                  const int32_t* __restrict__ perm,
+                                                  const int32_t* __restrict__ seg_offsets,
+                                                  const double* __restrict__ W, double* __restrict__ T,
+                                                  const double* __restrict__ ED, double kT, double eta,
+                                                  int32_t iters, double* __restrict__ cost, double* __restrict__ C,
+                                                  int32_t* __restrict__ status) {
+    using CH = Chain<M>;
+    constexpr int NE = CH::NE;
+    constexpr int NW = (M + 1) * 3;
+    const int lane = threadIdx.x;
+    const int slot = lane >> 1;
+    const bool right = lane & 1;
+    const int64_t i0 = blk * TPW;
+    const int nb = (int)((n - i0) < TPW ? (n - i0) : TPW);
+    const bool live = slot < nb;
+    if (lane < TPW) {
+        sm.in.bad[lane] = 0;
+        sm.in.base[lane] = 0;
+    }
+    __syncthreads();
+    int32_t b = 0;
+    int64_t s0 = 0;
+    if (live) {
+        b = perm[i0 + slot];
+        s0 = seg_offsets[b];
+        if (!right) sm.in.base[slot] = s0 * 24;
+        const double* gW = W + (s0 + b) * 3;
+        for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
+        for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
+    }
+    // this lane updates the times of its half of the segments; between steps they live
+    // in the stage only (an invalid trajectory keeps its times: its stage row was
+    // sanitised, so the cost reads them from memory, and nothing is written back)
+    const int nmine = right ? CH::nR : NE;
+    __syncthreads();
+    sanitize(sm.in, lane);
+    __syncthreads();
+    const bool valid = sm.in.bad[slot] == 0;
+    const double* ed = (HAS_ED && live) ? ED + (int64_t)b * 18 : ED;
+    int32_t st_last = TGMS_OK;
+    for (int32_t it = 0; it <= iters; ++it) {  // it == iters: the cost at the final times
+        const LaneView L = make_view<M>(sm.in, slot, right);
+        GradAcc<NE> G;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+        const int32_t st = pair_solve<M, HAS_ED, GradAcc<NE>>(L, right, valid, ed, G);
+        st_last = st;
+        double Fl = 0.0;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            if (live && e < nmine) {
+                const int phys = right ? M - 1 - e : e;
+                const double tl = valid ? sm.in.T[phys * PSTRIDE + slot] : T[s0 + phys];
+                Fl += G.J[e] + kT * tl;
+            }
+        }
+        const double F = Fl + pair_swap(Fl);
+        if (it == iters) {
+            if (live && !right && cost) cost[b] = F;
+            break;
+        }
+        const bool ok = (st == TGMS_OK) && F > 0.0;
+        __syncthreads();  // every lane has read the stage before the times change
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            if (live && valid && e < nmine) {
+                const int phys = right ? M - 1 - e : e;
+                const double tl = sm.in.T[phys * PSTRIDE + slot];
+                double dtau = -eta * tl * (G.dJ[e] + kT) / F;
+                dtau = fmin(fmax(dtau, -0.5), 0.5);
+                const double tn = ok ? tl * exp(dtau) : tl;
+                sm.in.T[phys * PSTRIDE + slot] = tn;
+                sm.in.R[phys * PSTRIDE + slot] = fast_rcp(tn);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        if (live && valid && e < nmine) {
+            const int phys = right ? M - 1 - e : e;
+            T[s0 + phys] = sm.in.T[phys * PSTRIDE + slot];
+        }
+    }
+    if (C) {
+        __syncthreads();
+        const LaneView L = make_view<M>(sm.in, slot, right);
+        const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
+        const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, ed, O);
+        if (live && !right && status) status[b] = st;
+    } else if (live && !right && status) {
+        status[b] = st_last;
+    }
+}
+
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_ragged(int32_t n, const int32_t* __restrict__ perm,
                                                                        const int32_t* __restrict__ seg_offsets,
@@ -2356,6 +2459,35 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_multi(GroupTable
         if constexpr (mm >= MLO && mm <= MHI)                                                              \
             refine_ragged_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g], \
                                             seg_offsets, W, T, ED, kT, eta, Tout, cost, status);           \
+        break;
+        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
+        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
+        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
+        TGMS_MULTI_CASE(16)
+#undef TGMS_MULTI_CASE
+        default: break;
+    }
+}
+
+template <int MLO, int MHI, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(GroupTable tab,
+                                                                            const int32_t* __restrict__ seg_offsets,
+                                                                            const double* __restrict__ W,
+                                                                            double* __restrict__ T,
+                                                                            const double* __restrict__ ED, double kT,
+                                                                            double eta, int32_t iters,
+                                                                            double* __restrict__ cost,
+                                                                            double* __restrict__ C,
+                                                                            int32_t* __restrict__ status) {
+    __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
+    int64_t blk;
+    const int g = group_of(tab, blockIdx.x, blk);
+    switch (tab.m[g]) {
+#define TGMS_MULTI_CASE(mm)                                                                                    \
+    case mm:                                                                                                  \
+        if constexpr (mm >= MLO && mm <= MHI)                                                                 \
+            refine_loop_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g],     \
+                                          seg_offsets, W, T, ED, kT, eta, iters, cost, C, status);           \
         break;
         TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
         TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
@@ -2469,6 +2601,29 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
 }
 
 }  // namespace
+
+template <int MLO, int MHI>
+hipError_t loop_multi_launch(const GroupTable& tab, const int32_t* so, const double* W, double* T, const double* ED,
+                             double kT, double eta, int32_t iters, double* cost, double* C, int32_t* status,
+                             hipStream_t stream) {
+    const unsigned grid = tab.ngroups ? (unsigned)tab.blk_end[tab.ngroups - 1] : 0u;
+    if (grid == 0) return hipSuccess;
+    if (ED)
+        hipLaunchKernelGGL((k_refine_loop_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+                           ED, kT, eta, iters, cost, C, status);
+    else
+        hipLaunchKernelGGL((k_refine_loop_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+                           ED, kT, eta, iters, cost, C, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* so, const double* W, double* T,
+                                    const double* ED, double kT, double eta, int32_t iters, double* cost, double* C,
+                                    int32_t* status, hipStream_t stream) {
+    if (cls == 0)
+        return loop_multi_launch<1, TGMS_TWO_WAVE_MAX_M>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    return loop_multi_launch<TGMS_TWO_WAVE_MAX_M + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+}
 
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
                                const double* T, const double* ED, double kT, double eta, double* Tout, double* cost,
