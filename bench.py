@@ -14,6 +14,7 @@ collective).  Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -402,8 +403,15 @@ def main():
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
+    # the timed launch with its arguments bound once (the C-ABI call and nothing else)
+    _solve = solver._L.tgms_solve_uniform_device
+    _args = (solver._h, B, M, dW.data_ptr(), dT.data_ptr(), None, dC.data_ptr(), dS.data_ptr(),
+             ctypes.c_void_p(sp))
+
     def step():
-        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+        st = _solve(*_args)
+        if st != 0:
+            raise RuntimeError(f"tgms_solve_uniform_device: status {st}: {solver.last_error()}")
 
     def barrier():
         if world > 1:
