@@ -430,15 +430,20 @@ def main():
     # launch duration is their elapsed time / K.  --graph 0: K Python-level launches.
     graph = None
     if args.graph:
-        cap = torch.cuda.Stream()
-        cap.wait_stream(stream)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=cap):
-            for _ in range(K):
-                solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=cap.cuda_stream)
-        stream.wait_stream(cap)
-        graph.replay()  # warm replay (graph upload)
-        torch.cuda.synchronize()
+        try:
+            cap = torch.cuda.Stream()
+            cap.wait_stream(stream)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=cap):
+                for _ in range(K):
+                    solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=cap.cuda_stream)
+            stream.wait_stream(cap)
+            graph.replay()  # warm replay (graph upload)
+            torch.cuda.synchronize()
+        except Exception as exc:  # capture unsupported here: time the Python loop instead
+            print(f"bench: HIP graph capture failed ({exc}); timing the launch loop", file=sys.stderr)
+            graph = None
+            torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
