@@ -434,7 +434,9 @@ def main():
             cap = torch.cuda.Stream()
             cap.wait_stream(stream)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=cap):
+            # thread-local capture: other threads (the RCCL process group's watchdog at
+            # N > 1) may keep making HIP calls while this thread captures
+            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
                 for _ in range(K):
                     solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=cap.cuda_stream)
             stream.wait_stream(cap)
