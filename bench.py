@@ -7,9 +7,13 @@
 
 One "step" = one solve of one batch of B = 65,536 synthetic trajectories (M = 10)
 per GPU (BASELINE.json configs[2] / SURVEY.md §8(d) config 3), inputs resident in
-HBM when the timed region starts, coefficients written to HBM.  Trajectories are
-independent, so N GPUs each solve their own shard (weak scaling, no data-path
-collective).  Rank 0 prints ONE JSON line.
+HBM when the timed region starts, coefficients written to HBM.  Every step solves a
+FRESH batch: the K steps rotate over `--sets` (4) independent batches, 594 MB per
+GPU, so no step finds its inputs or its output lines in the 256 MiB Infinity Cache
+where the step before left them (the same-batch loop, whose 148.6 MB stay on-die, is
+reported beside it as `cache_resident`).  Trajectories are independent, so N GPUs
+each solve their own shard (weak scaling, no data-path collective).  Rank 0 prints
+ONE JSON line.
 """
 from __future__ import annotations
 
@@ -48,16 +52,38 @@ def dense_flops_per_traj(M: int) -> float:
     return 2.0 / 3.0 * N ** 3 + 6.0 * N ** 2
 
 
+TRAFFIC_FILE = "profiles/pmc_traffic.json"
+
+
 def load_traffic(workload_key: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """Per-launch HBM bytes of this workload from the committed rocprofv3 PMC passes
+    (scripts/gpu_profile.sh -> scripts/pmc_traffic.py -> profiles/pmc_traffic.json):
+    PMC counters cannot be read inside this process, so the line reports the
+    committed measurement of the same command and names its source.  None if absent."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
             d = json.load(f)
         e = d.get(workload_key)
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         return None
+
+
+def available_cores() -> dict:
+    """Host cores this process may use: the affinity mask, capped by the cgroup CPU
+    quota (a container's share of a larger machine), as used by the CPU baseline."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota) if quota else aff}
 
 
 def _cpu_model() -> str:
@@ -70,50 +96,77 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _timed_reps(fn, n_per_call: int, target_s: float):
+    """Repeat fn() until about target_s of work is done; returns (items/s, reps, seconds)."""
+    t0 = time.perf_counter()
+    fn()
+    pilot = max(time.perf_counter() - t0, 1e-6)
+    reps = max(1, int(round(target_s / pilot)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    el = time.perf_counter() - t0
+    return n_per_call * reps / el, reps, el
+
+
 def cpu_baseline(B: int, M: int, target_s: float):
-    """The CPU oracle (build's own fp64 dense-KKT restatement; the reference has no
-    solver) on a bounded sample of the same workload, timed on this host."""
+    """CPU restatement of the solve (the reference has no solver to time, SURVEY.md §0,
+    §8(d)): the oracle's fp64 C code with OpenMP over trajectories, on every core this
+    process may use, on a bounded sample of the same workload.  `value` is its reduced
+    formulation (the GPU kernel's math, O(M) per trajectory: the strongest CPU
+    restatement); the survey's literal dense-KKT LU and the one-core rates are beside it."""
     from oracle import oracle as O
     from trajectory_generator_ros2_amd import synthetic as S
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "1") or 1)
+    cores = available_cores()
+    threads = cores["usable"]
     so, W, T = S.uniform_batch(B, M)
-    # pilot on a slice, then repeat the whole per-GPU batch (or a prefix of it) until
-    # about target_s of CPU work has been done
-    t0 = time.perf_counter()
-    O.solve_batch(so[:1025], W[:1024], T[:1024], None, O.KKT_C4, threads)
-    pilot = max(time.perf_counter() - t0, 1e-6) / 1024.0
-    n_batch = int(min(B, max(1024, target_s / pilot)))
-    reps = max(1, int(round(target_s / (pilot * n_batch))))
-    so_n = so[: n_batch + 1]
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        _, st = O.solve_batch(so_n, W[:n_batch], T[:n_batch], None, O.KKT_C4, threads)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+
+    def reduced():
+        _, st = O.solve_batch(so, W, T, None, O.REDUCED, threads)
         assert (st == 0).all()
-    el = time.perf_counter() - t0
-    n = n_batch * reps
-    # single-core rate on a 2048-trajectory slice (SURVEY §8(d): 1 core and all cores)
+
+    red_rate, red_reps, red_s = _timed_reps(reduced, B, 0.6 * target_s)
+    # dense KKT on a prefix sized to ~0.4 target_s
+    n = 4096
+    so_n = so[: n + 1]
+
+    def dense():
+        _, st = O.solve_batch(so_n, W[: n * (M + 1)], T[: n * M], None, O.KKT_C4, threads)
+        assert (st == 0).all()
+
+    dense_rate, dense_reps, dense_s = _timed_reps(dense, n, 0.4 * target_s)
     t1 = time.perf_counter()
-    O.solve_batch(so[:2049], W[:2048], T[:2048], None, O.KKT_C4, 1)
-    one_core = 2048 / (time.perf_counter() - t1)
-    # the same threads on the reduced formulation (the GPU kernel's math, O(M) per
-    # trajectory): the strongest CPU restatement, beside the survey's dense-KKT one
-    t2 = time.perf_counter()
-    _, st = O.solve_batch(so, W, T, None, O.REDUCED, threads)
-    assert (st == 0).all()
-    reduced = B / (time.perf_counter() - t2)
-    return {"value": n / el, "unit": "trajectories/s", "cores": threads, "kind": "port",
-            "value_1core": one_core, "value_reduced_formulation": reduced, "cpu_model": _cpu_model(),
-            "sample": f"{reps} x {n_batch} trajectories of the config-3 workload (M={M}), oracle dense KKT "
-                      f"(LU, partial pivoting, fp64), {threads} OpenMP thread(s), {el:.1f} s"}
+    O.solve_batch(so[:8193], W[: 8192 * (M + 1)], T[: 8192 * M], None, O.REDUCED, 1)
+    red_1 = 8192 / (time.perf_counter() - t1)
+    t1 = time.perf_counter()
+    O.solve_batch(so[:1025], W[: 1024 * (M + 1)], T[: 1024 * M], None, O.KKT_C4, 1)
+    dense_1 = 1024 / (time.perf_counter() - t1)
+    return {"value": red_rate, "unit": "trajectories/s", "cores": threads, "kind": "port",
+            "what": "cpu_restatement (reference has no solver): oracle/minsnap_oracle.c, fp64, OpenMP",
+            "cores_detail": cores, "cpu_model": _cpu_model(),
+            "value_1core": red_1, "dense_kkt_value": dense_rate, "dense_kkt_value_1core": dense_1,
+            "sample": f"reduced formulation: {red_reps} x {B} trajectories of the config-3 workload (M={M}), "
+                      f"{red_s:.1f} s; dense KKT (LU, partial pivoting): {dense_reps} x {n}, {dense_s:.1f} s; "
+                      f"{threads} OpenMP thread(s)"}
 
 
-def config5_line(solver, B, dev, stream, iters=10, k_T=1.0, eta=0.1, reps=3):
-    """Config 5 per GPU: ragged batch (M ~ U{2..16}) + `iters` time-refinement steps
-    + the final solve, one tgms_refine_loop_device call (planned once)."""
+def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_T=1.0, eta=0.1, reps=3):
+    """Config 5: a 1,048,576-trajectory ragged batch (M ~ U{2..16}) split over `world`
+    GPUs into contiguous cost-balanced shards (shard.ragged_bounds over 8 shards, the
+    configuration's GPU count, whatever N is); this rank solves shard `rank % 8`:
+    `iters` time-refinement steps + the final solve, one tgms_refine_loop_device call
+    (planned once)."""
     import torch
+    from trajectory_generator_ros2_amd import shard as SH
     from trajectory_generator_ros2_amd import synthetic as S
-    so, W, T = S.ragged_batch(B, 2, 16)
+    so_all, W_all, T_all = S.ragged_batch(B_total, 2, 16)
+    bounds = SH.ragged_bounds(so_all, 8)
+    part = rank % 8
+    so, W, T, _ = SH.shard_csr(so_all, W_all, T_all, None, int(bounds[part]), int(bounds[part + 1]))
+    del so_all, W_all, T_all
+    B = len(so) - 1
     d_so = torch.from_numpy(so.astype(np.int32)).to(dev)
     dW = torch.from_numpy(W.reshape(-1, 3)).to(dev)
     T0 = torch.from_numpy(T.reshape(-1)).to(dev)
@@ -133,7 +186,8 @@ def config5_line(solver, B, dev, stream, iters=10, k_T=1.0, eta=0.1, reps=3):
         run()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / reps * 1e3
-    return {"workload": f"config5: {B} ragged trajectories/GPU, M~U{{2..16}}, {iters} refinement steps + final solve",
+    return {"workload": f"config5: shard {part} of 8 (cost-balanced, {B} trajectories) of a {B_total}-trajectory "
+                        f"ragged batch, M~U{{2..16}}, {iters} refinement steps + final solve",
             "ms_per_batch": ms, "trajectories_per_s": B / (ms * 1e-3), "segments": int(so[-1]),
             "k_T": k_T, "eta": eta}
 
@@ -214,39 +268,26 @@ def config4_line(solver, M, dev, stream, world, rank, B=131072, chunks=8, reps=3
     return line
 
 
-def rotating_line(solver, B, M, dev, stream, sets=4, K=40):
-    """The headline launch with a fresh batch every step: `sets` independent batches
-    (inputs and outputs, 4 x 148.6 MB at config 3) are solved in turn, so no launch
-    finds its data in the 256 MB Infinity Cache left there by the previous one (the
-    headline loop re-solves one batch whose 148.6 MB stay on-die).  Reported beside
-    `value`, never as it."""
+def cache_resident_line(solver, B, M, buf, stream, K=40):
+    """The same launch re-solving ONE batch K times: its 148.6 MB (inputs + output)
+    stay in the 256 MiB Infinity Cache between launches, so the coefficient stores
+    merge on-die.  A kernel-benchmark figure, reported beside the headline (which
+    rotates over fresh batches), never as it."""
     import torch
-    from trajectory_generator_ros2_amd import synthetic as S
-    bufs = []
-    for i in range(sets):
-        _, W, T = S.uniform_batch(B, M, seed=S.SEED + 1000 + i)
-        bufs.append((torch.from_numpy(W).to(dev), torch.from_numpy(T).to(dev),
-                     torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev),
-                     torch.zeros((B,), dtype=torch.int32, device=dev)))
+    dW, dT, dC, dS = buf
     sp = stream.cuda_stream
-
-    def step(k):
-        dW, dT, dC, dS = bufs[k % sets]
-        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
-
-    for k in range(sets):
-        step(k)
+    solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    for k in range(K):
-        step(k)
+    for _ in range(K):
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
     e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / K
-    assert all(int((b[3] != 0).sum().item()) == 0 for b in bufs), "solver reported failures"
+    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
     gbs = algorithmic_bytes_per_traj(M) * B / (ms * 1e-3) / 1e9
-    return {"sets": sets, "working_set_MB": sets * algorithmic_bytes_per_traj(M) * B / 1e6, "launch_ms": ms,
+    return {"working_set_MB": algorithmic_bytes_per_traj(M) * B / 1e6, "launch_ms": ms,
             "trajectories_per_s": B / (ms * 1e-3), "achieved_GBs": gbs, "frac_of_peak": gbs / HBM_PEAK_GBS}
 
 
@@ -358,6 +399,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
     ap.add_argument("--segments", type=int, default=10)
+    ap.add_argument("--sets", type=int, default=4,
+                    help="independent batches the timed steps rotate over (a fresh batch every step)")
     ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the K timed steps replayed from one captured HIP graph; 0: K Python-level launches")
@@ -366,8 +409,8 @@ def main():
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
     ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
-    ap.add_argument("--rotating", type=int, default=1,
-                    help="side line: a fresh batch every launch (4 batches, beyond the Infinity Cache): 1/0")
+    ap.add_argument("--cache-resident", type=int, default=1,
+                    help="side line: the same batch every launch (its 148.6 MB stay in the Infinity Cache): 1/0")
     ap.add_argument("--config4", type=int, default=1,
                     help="config-4 side line (131,072/GPU, pipelined RCCL gather to rank 0 when N > 1): 1/0")
     ap.add_argument("--node-line", type=int, default=1, help="config-1 node-path latency side line: 1/0")
@@ -391,25 +434,30 @@ def main():
     from trajectory_generator_ros2_amd import synthetic as S
     from trajectory_generator_ros2_amd.solver import Solver
 
-    B, M = args.batch, args.segments
+    B, M, sets = args.batch, args.segments, max(1, args.sets)
     dev = torch.cuda.current_device()
     solver = Solver(dev, METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
-    # this rank's shard of the job: independent trajectories, seed offset by rank
-    _, W, T = S.uniform_batch(B, M, seed=S.SEED + rank)
-    dW = torch.from_numpy(W).to(dev)
-    dT = torch.from_numpy(T).to(dev)
-    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev)
-    dS = torch.empty((B,), dtype=torch.int32, device=dev)
+    # this rank's shard of the job: `sets` independent batches of independent
+    # trajectories (set 0: seed + rank, as every side line uses)
+    bufs = []
+    for i in range(sets):
+        _, Wi, Ti = S.uniform_batch(B, M, seed=S.SEED + rank + 7919 * i)
+        if i == 0:
+            W, T = Wi, Ti
+        bufs.append((torch.from_numpy(Wi).to(dev), torch.from_numpy(Ti).to(dev),
+                     torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev),
+                     torch.full((B,), -1, dtype=torch.int32, device=dev)))
+    dW, dT, dC, dS = bufs[0]
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
-    # the timed launch with its arguments bound once (the C-ABI call and nothing else)
+    # the timed launches with their arguments bound once (the C-ABI call and nothing else)
     _solve = solver._L.tgms_solve_uniform_device
-    _args = (solver._h, B, M, dW.data_ptr(), dT.data_ptr(), None, dC.data_ptr(), dS.data_ptr(),
-             ctypes.c_void_p(sp))
+    _args = [(solver._h, B, M, b[0].data_ptr(), b[1].data_ptr(), None, b[2].data_ptr(), b[3].data_ptr(),
+              ctypes.c_void_p(sp)) for b in bufs]
 
-    def step():
-        st = _solve(*_args)
+    def step(k):
+        st = _solve(*_args[k % sets])
         if st != 0:
             raise RuntimeError(f"tgms_solve_uniform_device: status {st}: {solver.last_error()}")
 
@@ -417,18 +465,26 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    def all_ranks(x: float, op):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    for k in range(max(args.warmup, sets)):
+        step(k)
     torch.cuda.synchronize()
-    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+    assert all(int((b[3] != 0).sum().item()) == 0 for b in bufs), "solver reported failures"
 
     K = args.steps
     # The K steps are captured once into a HIP graph (torch.cuda.CUDAGraph over the
     # library's launches) and replayed as one submission, so a slow or busy host cannot
-    # starve the GPU between ~25 us launches; every step is still one full solve of the
+    # starve the GPU between ~30 us launches; every step is still one full solve of a
     # batch.  HIP events on the launch stream bracket the timed region; the average
     # launch duration is their elapsed time / K.  --graph 0: K Python-level launches.
-    graph = None
+    # Every rank times the same launch mode: if capture fails on any rank, all fall back.
+    graph, capture_error = None, None
     if args.graph:
         try:
             cap = torch.cuda.Stream()
@@ -437,15 +493,19 @@ def main():
             # thread-local capture: other threads (the RCCL process group's watchdog at
             # N > 1) may keep making HIP calls while this thread captures
             with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
-                for _ in range(K):
-                    solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=cap.cuda_stream)
+                for k in range(K):
+                    dWk, dTk, dCk, dSk = bufs[k % sets]
+                    solver.solve_uniform_device(B, M, dWk, dTk, dCk, dSk, stream=cap.cuda_stream)
             stream.wait_stream(cap)
             graph.replay()  # warm replay (graph upload)
             torch.cuda.synchronize()
         except Exception as exc:  # capture unsupported here: time the Python loop instead
-            print(f"bench: HIP graph capture failed ({exc}); timing the launch loop", file=sys.stderr)
+            capture_error = f"{type(exc).__name__}: {exc}"
+            print(f"bench: HIP graph capture failed ({capture_error}); timing the launch loop", file=sys.stderr)
             graph = None
             torch.cuda.synchronize()
+        if all_ranks(1.0 if graph is not None else 0.0, dist.ReduceOp.MIN if world > 1 else None) < 1.0:
+            graph = None  # some rank could not capture: every rank times the launch loop
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
@@ -455,18 +515,25 @@ def main():
     if graph is not None:
         graph.replay()
     else:
-        for _ in range(K):
-            step()
+        for k in range(K):
+            step(k)
     ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = all_ranks(time.perf_counter() - t0, dist.ReduceOp.MAX if world > 1 else None)
     launch_ms = ev0.elapsed_time(ev1) / K
-    assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+    launch_ms_max = all_ranks(launch_ms, dist.ReduceOp.MAX if world > 1 else None)
+    launch_ms_min = all_ranks(launch_ms, dist.ReduceOp.MIN if world > 1 else None)
+    assert all(int((b[3] != 0).sum().item()) == 0 for b in bufs), "solver reported failures"
+    launch_mode = "hip_graph_of_K_steps" if graph is not None else "python_loop"
+    del graph
+
+    cache_res = None
+    if args.cache_resident and args.method == "reduced":
+        cache_res = cache_resident_line(solver, B, M, bufs[0], stream)
+    # the side lines use set 0 only
+    del bufs, _args
+    torch.cuda.empty_cache()
 
     # dense-KKT side line (the survey's literal formulation), same inputs, same GPU
     dense = None
@@ -488,6 +555,7 @@ def main():
                  "fp64_tflops_algorithmic": gfl, "fp64_peak_tflops": FP64_PEAK_TFS,
                  "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
+        del dC2
 
     # band-KKT side line: the same literal KKT and partial-pivoting LU in the order in
     # which it is banded (tgms_band.hip), same inputs, same GPU
@@ -511,14 +579,11 @@ def main():
                 "flops_per_traj": band_flops_per_traj(M), "fp64_peak_tflops": FP64_PEAK_TFS,
                 "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_REDUCED)
+        del dC3
 
     config5 = None
     if args.config5 and M == 10:
-        config5 = config5_line(solver, B, dev, stream)
-
-    rotating = None
-    if args.rotating and args.method == "reduced":
-        rotating = rotating_line(solver, B, M, dev, stream)
+        config5 = config5_line(solver, dev, stream, world, rank)
 
     config4 = None
     if args.config4 and M == 10:
@@ -536,14 +601,16 @@ def main():
     if args.node_line and rank == 0:
         node = node_line()
 
+    # rank-0-only host work, after every GPU timing (the other ranks wait at the
+    # final barrier)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         cpu = cpu_baseline(B, M, args.cpu_seconds)
 
     if rank == 0:
         bpl = algorithmic_bytes_per_traj(M) * B
-        achieved = bpl / (launch_ms * 1e-3) / 1e9
-        key = f"B{B}_M{M}_{args.method}"
+        achieved = bpl / (launch_ms_max * 1e-3) / 1e9
+        key = f"B{B}_M{M}_{args.method}_sets{sets}"
         traffic = load_traffic(key)
         value = world * B * K / el
         line = {
@@ -558,30 +625,38 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md 8(d): seed 20251015+rank, room-bound uniform waypoints, "
-                    "T=clip(|dw|/1m/s,0.5,10), rest-to-rest)",
+            "data": "synthetic (SURVEY.md 8(d): seed 20251015+rank(+7919 i for batch i), room-bound uniform "
+                    "waypoints, T=clip(|dw|/1m/s,0.5,10), rest-to-rest)",
             "config": {"workload": f"config3: {B} trajectories/GPU x {M} segments, order 7, 3 axes, "
-                                   f"coefficients [traj][seg][axis][8] fp64 in HBM",
-                       "batch_per_gpu": B, "segments": M, "method": args.method,
-                       "launch": "hip_graph_of_K_steps" if graph is not None else "python_loop",
+                                   f"coefficients [traj][seg][axis][8] fp64 in HBM; a fresh batch every step "
+                                   f"({sets} batches rotated, {sets * bpl / 1e6:.0f} MB per GPU)",
+                       "batch_per_gpu": B, "segments": M, "sets": sets, "method": args.method,
+                       "launch": launch_mode,
                        "parallelism": f"shard{world} (independent trajectories, no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
+                         "traffic_source": (f"{TRAFFIC_FILE}[{key}]: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                            f"passes of this command (scripts/gpu_profile.sh), not this run")
+                         if traffic is not None else None,
                          "kernel": f"k_reduced_uniform<{M}>" if args.method == "reduced" else f"k_dense_kkt<{M}>",
-                         "launch_ms": launch_ms,
+                         "launch_ms": launch_ms_max,
+                         "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
                          "algorithmic_bytes_per_launch": bpl},
             "cpu_baseline": cpu,
+            "cache_resident": cache_res,
             "dense_kkt": dense,
             "band_kkt": band,
             "sampler": sampler,
-            "rotating_batches": rotating,
             "config4": config4,
             "config5": config5,
             "host_path": host,
             "node_config1": node,
         }
+        if capture_error is not None:
+            line["config"]["graph_capture_error"] = capture_error
         print(json.dumps(line), flush=True)
+    barrier()
     solver.close()
     if world > 1:
         dist.destroy_process_group()

@@ -24,7 +24,10 @@
  *     reference calls from its single rclcpp executor thread,
  *     src/trajectory_generator_node.cpp:30);
  *   - `*_device` entry points take device pointers and a hipStream_t passed as
- *     void* and are asynchronous; the others take host pointers and block;
+ *     void* and are asynchronous; the others take host pointers and block.  Calls
+ *     of one handle that use its device scratch (ragged plans, the refinement loop,
+ *     the band-KKT method) may be issued on different streams: the handle orders
+ *     them on the GPU with an event (each waits for the previous one's work);
  *     fp64 device arrays must be 16-byte aligned (TGMS_ERR_INVALID_ARG otherwise;
  *     hipMalloc allocations are, a slice at an odd element offset is not);
  *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
@@ -32,7 +35,7 @@
  *
  * Layouts (fp64, row-major, trajectory-major).  A batch is CSR over segments:
  * trajectory b has M_b = seg_offsets[b+1] - seg_offsets[b] segments (1..TGMS_MAX_SEGMENTS):
- *   seg_offsets  int32 [B+1], seg_offsets[0] = 0, non-decreasing
+ *   seg_offsets  int32 [B+1], seg_offsets[0] = 0, strictly increasing (1 <= M_b <= max)
  *   waypoints    [sum_b (M_b+1)][3]   rows of b start at seg_offsets[b] + b
  *   seg_times    [sum_b M_b]          T_i > 0 and finite, starting at seg_offsets[b]
  *   end_derivs   NULL (rest-to-rest, as every reference primitive starts and ends
@@ -73,8 +76,8 @@ typedef enum tgms_method {
                                  segment-interleaved order where it is banded (kl = ku = 9);
                                  the structurally-zero entries are skipped, half a wavefront
                                  per trajectory, M <= TGMS_MAX_SEGMENTS.  Its U rows live in a
-                                 handle-owned scratch slab: solves of one handle on different
-                                 streams must not overlap in time */
+                                 handle-owned scratch slab (calls of one handle on different
+                                 streams are serialised on the GPU) */
 } tgms_method;
 
 typedef enum tgms_yaw_mode {

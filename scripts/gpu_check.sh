@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
 ok() { local c=$1; [ "$c" -eq 0 ] || [ "$c" -eq 1 ]; }   # 1 = test failure, keep going
-SIDE_OFF="--dense-steps 0 --band-steps 0 --sample-traj 0 --config5 0 --config4 0 --rotating 0 --host-line 0 --node-line 0"
+SIDE_OFF="--dense-steps 0 --band-steps 0 --sample-traj 0 --config5 0 --config4 0 --cache-resident 0 --host-line 0 --node-line 0"
 
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; c=$?
 echo "pytest exit $c"; tail -5 $OUT/pytest_gpu.log
@@ -22,7 +22,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-
     python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 $SIDE_OFF > $OUT/prof_bench.json 2> $OUT/prof.err; c=$?
 echo "rocprof (headline) exit $c"
 [ $c -eq 0 ] || exit $c
-# every side line (dense KKT, sampler, config 4/5, rotating batches, host and node paths)
+# every side line (dense KKT, sampler, config 4/5, cache-resident loop, host and node paths)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_full -o run --output-format csv -- \
     python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 --dense-steps 2 > $OUT/prof_full_bench.json 2> $OUT/prof_full.err; c=$?
 echo "rocprof (full) exit $c"

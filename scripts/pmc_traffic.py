@@ -7,7 +7,7 @@ HBM section prescribes for gfx950:
   WRITE_SIZE (KB) is exact for 16-B-per-lane streaming stores
 Each counter comes from its own --pmc pass (they cannot share one).
 
-usage: pmc_traffic.py [gpurun_out/pmc] [key]      key e.g. B65536_M10_reduced
+usage: pmc_traffic.py [gpurun_out/pmc] [key]      key e.g. B65536_M10_reduced_sets4
 """
 import collections
 import csv
@@ -30,7 +30,7 @@ def per_dispatch(pmc_dir, kernel_substr):
 
 def main():
     pmc_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
-    key = sys.argv[2] if len(sys.argv) > 2 else "B65536_M10_reduced"
+    key = sys.argv[2] if len(sys.argv) > 2 else "B65536_M10_reduced_sets4"
     kernel = "k_reduced_uniform" if "reduced" in key else "k_dense_kkt"
     mean, n = per_dispatch(pmc_dir, kernel)
     if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:

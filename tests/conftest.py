@@ -56,3 +56,41 @@ def batch_rel_err(so, C, R):
     rm = np.maximum.reduceat(r, so[:-1], axis=0)
     rm = np.where(rm == 0.0, 1.0, rm)
     return float((dm / rm).max())
+
+
+def _deriv(c, t, k):
+    """k-th derivative of sum_j c_j t^j (c [..., 8], t broadcastable to c[..., 0])."""
+    j = np.arange(8)
+    f = np.array([np.prod(np.arange(jj - k + 1, jj + 1)) if jj >= k else 0.0 for jj in j])
+    p = np.where(j >= k, j - k, 0)
+    return (c * f * np.power(np.asarray(t)[..., None], p)).sum(-1)
+
+
+def check_spline_properties(so, W, T, C, atol_pos=1e-8, rtol_cont=1e-7):
+    """Size-independent properties of a rest-to-rest min-snap solution of a CSR batch
+    (every trajectory, any size): c0 = start waypoint and p(T) = end waypoint of every
+    segment, derivatives 1..6 continuous at every interior knot, v = a = j = 0 at both
+    ends.  so [B+1], W [S+B,3], T [S], C [S,3,8]."""
+    so = np.asarray(so, dtype=np.int64)
+    B = so.shape[0] - 1
+    S = int(so[-1])
+    W = np.asarray(W).reshape(-1, 3)
+    T = np.asarray(T).reshape(-1)
+    C = np.asarray(C).reshape(S, 3, 8)
+    Ms = np.diff(so)
+    traj = np.repeat(np.arange(B), Ms)
+    rows = np.arange(S) + traj                     # start waypoint row of every segment
+    np.testing.assert_allclose(C[..., 0], W[rows], rtol=0, atol=1e-12)
+    Tt = np.repeat(T[:, None], 3, axis=1)          # [S,3]
+    np.testing.assert_allclose(_deriv(C, Tt, 0), W[rows + 1], rtol=0, atol=atol_pos)
+    first = so[:-1]
+    last = so[1:] - 1
+    inner = np.setdiff1d(np.arange(S - 1), last)  # segment s and s+1 in one trajectory
+    for k in range(1, 7):
+        left = _deriv(C[inner], Tt[inner], k)
+        right = _deriv(C[inner + 1], 0.0 * Tt[inner + 1], k)
+        scale = np.abs(right).max() + 1.0 if right.size else 1.0
+        assert np.abs(left - right).max(initial=0.0) <= rtol_cont * scale, k
+    for k in range(1, 4):
+        assert np.abs(C[first, :, k]).max() == 0.0
+        assert np.abs(_deriv(C[last], Tt[last], k)).max() <= atol_pos

@@ -1,0 +1,118 @@
+"""GPU parity at the BASELINE configurations' own sizes.
+
+* config 2: B = 1,024 x M = 3, every trajectory against the oracle;
+* config 4's per-GPU shard: 131,072 x M = 10 through the device API.  Its output
+  (252 MB) is above the streaming-store switch of the uniform kernel (192 MiB), so this
+  is the store path config 4 runs;
+* config 5's per-GPU share: rank 0's cost-balanced shard of a 1,048,576-trajectory ragged
+  batch (M ~ U{2..16}, shard.ragged_bounds over 8 ranks, ~131,072 trajectories), 10 time
+  refinement steps and the final solve through tgms_refine_loop_device.
+
+Checks: the oracle on slices of 1,024 trajectories (start, middle, end), and on every
+trajectory the size-independent properties of a min-snap spline (interpolation,
+C1..C6 continuity, rest ends: conftest.check_spline_properties).  Tolerances as
+everywhere: norm-wise 1e-9 per (trajectory, axis) for a solve; 1e-8 after 10 refinement
+steps (test_gpu_parity.py::test_refine_matches_oracle explains the margin).
+"""
+import numpy as np
+import pytest
+
+from conftest import batch_rel_err, check_spline_properties
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+REFINE_TOL = 1e-8
+
+
+def _slices(B, n=1024):
+    return [(0, n), (B // 2 - n // 2, B // 2 + n // 2), (B - n, B)]
+
+
+def test_config2_exact_size(solver, oracle):
+    """BASELINE config 2 (1,024 x M = 3) through the host and the device API."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    B, M = 1024, 3
+    so, W, T = S.uniform_batch(B, M)
+    Wf, Tf = W.reshape(-1, 3), T.reshape(-1)
+    C, st, worst = solver.solve(so, Wf, Tf)
+    assert worst == 0 and (st == 0).all()
+    R, rst = oracle.solve_batch(so, Wf, Tf, None, oracle.KKT_C4)
+    assert (rst == 0).all()
+    assert batch_rel_err(so, C, R) <= TOL
+    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+    dS = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    solver.solve_uniform_device(B, M, torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda(), dC, dS)
+    torch.cuda.synchronize()
+    assert np.array_equal(dC.cpu().numpy().reshape(-1, 3, 8), C)
+    assert (dS.cpu().numpy() == 0).all()
+    check_spline_properties(so, Wf, Tf, C)
+
+
+def test_config4_shard_streaming_store_path(solver, oracle):
+    """131,072 x M = 10 (one GPU's share of config 4): the uniform kernel's streaming
+    store path.  Oracle on three slices, properties on every trajectory, and the same
+    trajectories solved in a batch small enough for the regular store path agree bit
+    for bit."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    B, M = 131072, 10
+    assert B * M * 24 * 8 > (192 << 20)  # above the streaming-store switch
+    so, W, T = S.uniform_batch(B, M, seed=S.SEED + 3)
+    dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+    dC = torch.full((B, M, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+    dS = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    solver.solve_uniform_device(B, M, dW, dT, dC, dS)
+    torch.cuda.synchronize()
+    assert (dS.cpu().numpy() == 0).all()
+    C = dC.cpu().numpy()
+    Wf, Tf = W.reshape(-1, 3), T.reshape(-1)
+    for lo, hi in _slices(B):
+        so_l = so[: hi - lo + 1]
+        R, rst = oracle.solve_batch(so_l, W[lo:hi].reshape(-1, 3), T[lo:hi].reshape(-1), None, oracle.KKT_C4)
+        assert (rst == 0).all()
+        assert batch_rel_err(so_l, C[lo:hi].reshape(-1, 3, 8), R) <= TOL, (lo, hi)
+    check_spline_properties(so, Wf, Tf, C)
+    # the regular-store path (a 65,536 piece: 126 MB of output) gives the same bits
+    half = B // 2
+    dC2 = torch.empty((half, M, 3, 8), dtype=torch.float64, device="cuda")
+    solver.solve_uniform_device(half, M, dW[half:], dT[half:], dC2)
+    torch.cuda.synchronize()
+    assert torch.equal(dC2, dC[half:])
+
+
+def test_config5_per_gpu_share(solver, oracle):
+    """Rank 0's cost-balanced share of config 5 (1,048,576 ragged over 8 GPUs), 10
+    refinement steps + the final solve in one tgms_refine_loop_device call."""
+    import torch
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd import synthetic as S
+    so_all, W_all, T_all = S.ragged_batch(1048576, 2, 16)
+    bounds = SH.ragged_bounds(so_all, 8)
+    so, W, T, _ = SH.shard_csr(so_all, W_all, T_all, None, int(bounds[0]), int(bounds[1]))
+    del W_all, T_all
+    B = len(so) - 1
+    assert 120000 < B < 140000
+    k_T, eta, iters = 1.0, 0.1, 10
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so.astype(np.int32)), d(W), d(T.copy())
+    dC = torch.full((int(so[-1]), 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+    dcost = torch.empty(B, dtype=torch.float64, device="cuda")
+    dst = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    solver.refine_loop_device(so, dso, dW, dT, k_T, eta, iters, dC, dcost, dst)
+    torch.cuda.synchronize()
+    Tg, Cg, cg, stg = dT.cpu().numpy(), dC.cpu().numpy(), dcost.cpu().numpy(), dst.cpu().numpy()
+    assert (stg == 0).all()
+    assert np.isfinite(cg).all() and (cg > 0).all()
+    assert not np.array_equal(Tg, T)
+    for lo, hi in _slices(B):
+        so_l, W_l, T_l, _ = SH.shard_csr(so, W, T, None, lo, hi)
+        To, co, Co, sto = oracle.refine_batch(so_l, W_l, T_l, None, k_T, eta, iters, oracle.REDUCED)
+        assert (sto == 0).all()
+        s0, s1 = int(so[lo]), int(so[hi])
+        assert np.abs(Tg[s0:s1] / To - 1).max() <= REFINE_TOL, (lo, hi)
+        assert np.abs(cg[lo:hi] / co - 1).max() <= REFINE_TOL, (lo, hi)
+        assert batch_rel_err(so_l, Cg[s0:s1], Co) <= REFINE_TOL, (lo, hi)
+    # the final coefficients are the min-snap solve at the final times, for every trajectory
+    check_spline_properties(so, W, Tg, Cg)

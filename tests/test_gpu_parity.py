@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import batch_rel_err
+from conftest import batch_rel_err, check_spline_properties
 
 pytestmark = pytest.mark.gpu
 
@@ -179,26 +179,7 @@ def test_config3_full_size_properties(solver, oracle):
     R, _ = oracle.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, oracle.REDUCED)
     assert batch_rel_err(so, C, R) <= TOL
     # interpolation and C6 continuity at every interior knot, rest at both ends
-    Cb = C.reshape(B, M, 3, 8)
-    j = np.arange(8)
-    Tt = T.reshape(B, M, 1, 1)
-
-    def deriv(c, t, k):
-        f = np.array([np.prod(np.arange(jj - k + 1, jj + 1)) if jj >= k else 0.0 for jj in j])
-        p = np.where(j >= k, j - k, 0)
-        return (c * f * np.power(t, p)).sum(-1)
-
-    np.testing.assert_allclose(Cb[..., 0], W[:, :-1, :], rtol=0, atol=1e-12)
-    end_p = deriv(Cb, Tt, 0)
-    np.testing.assert_allclose(end_p, W[:, 1:, :], rtol=0, atol=1e-8)
-    for k in range(1, 7):
-        left = deriv(Cb[:, :-1], Tt[:, :-1], k)
-        right = deriv(Cb[:, 1:], 0.0 * Tt[:, 1:], k)
-        scale = np.abs(right).max() + 1.0
-        assert np.abs(left - right).max() <= 1e-7 * scale, k
-    for k in range(1, 4):
-        assert np.abs(Cb[:, 0, :, k]).max() == 0.0
-        assert np.abs(deriv(Cb[:, -1], Tt[:, -1], k)).max() <= 1e-8
+    check_spline_properties(so, W.reshape(-1, 3), T.reshape(-1), C)
 
 
 def test_device_ragged_matches_host(solver):

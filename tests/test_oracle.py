@@ -218,3 +218,20 @@ def test_sample_count_convention(oracle):
     assert oracle.sample_count(0.005, 0.01) == 2
     assert oracle.sample_count(0.0, 0.01) == 2
     assert oracle.sample_count(10.0, 0.1) == 101
+
+
+def test_spline_property_checker(oracle):
+    """conftest.check_spline_properties (used at full size on the GPU) accepts the
+    oracle's solution of a ragged batch and rejects a perturbed one."""
+    from conftest import check_spline_properties
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(200, 1, 16, seed=3)
+    C, st = oracle.solve_batch(so, W, T, None, oracle.REDUCED)
+    assert (st == 0).all()
+    check_spline_properties(so, W, T, C)
+    bad = C.copy()
+    bad[int(so[7]) + 1, 2, 5] += 1e-3  # a kink inside trajectory 7 (M >= 2 there?)
+    if so[8] - so[7] < 2:
+        bad[int(so[8]) - 1, 2, 5] += 1e-3
+    with pytest.raises(AssertionError):
+        check_spline_properties(so, W, T, bad)

@@ -247,9 +247,7 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
 #undef A_
 }
 
-#ifndef TGMS_BAND_LB
-#define TGMS_BAND_LB 1  // minimum wavefronts per SIMD the register allocation must allow
-#endif
+constexpr int TGMS_BAND_LB = 1;  // minimum wavefronts per SIMD the register allocation must allow
 
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
@@ -384,11 +382,7 @@ __global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, 
         double* xs = s_x[h];
         double* out = C + s0 * 24;
         double fin = 0.0;
-#ifdef TGMS_BAND_NOBACK  // diagnostic: forward elimination only
-        for (int k0 = -1; k0 >= 0; k0 -= PFB) {
-#else
         for (int k0 = kN; k0 >= 0; k0 -= PFB) {
-#endif
 #pragma unroll
             for (int s = 0; s < PFB; ++s) {
                 const int k = k0 - s;
@@ -462,12 +456,12 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
     const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, BAND_WAVES_PER_CU);
     const int32_t g = std::min<int32_t>(std::min(grid, resident), (n_traj + 1) / 2);
     if (ED)
-        hipLaunchKernelGGL((k_band_kkt<M, true>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
+        TGMS_LAUNCH((k_band_kkt<M, true>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
                            status, scratch);
     else
-        hipLaunchKernelGGL((k_band_kkt<M, false>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
+        TGMS_LAUNCH((k_band_kkt<M, false>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
                            status, scratch);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 }  // namespace

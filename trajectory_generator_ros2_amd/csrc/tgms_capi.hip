@@ -38,6 +38,16 @@ struct tgms_handle {
     int32_t* h_perm = nullptr;  // pinned staging of the plan
     size_t h_perm_cap = 0;
     hipEvent_t perm_ev = nullptr;  // guards h_perm reuse until the upload completed
+    // Handle-owned device scratch (d_perm, d_loop_ws, d_band) is in use by the work
+    // enqueued up to scratch_ev.  Every asynchronous entry point that touches it makes
+    // its stream wait for scratch_ev first and records it again after its own work, so
+    // calls on different streams are ordered on the GPU (no host blocking).
+    hipEvent_t scratch_ev = nullptr;
+    bool scratch_pending = false;
+    // tgms_refine_loop_device's second time buffer (kept apart from d_ws, which the
+    // blocking host API reuses)
+    double* d_loop_ws = nullptr;
+    size_t loop_ws_cap = 0;
     // ragged plans: the per-M group launches fork onto these streams and join back, so
     // the groups (each a few hundred wavefronts) run side by side instead of in series
     hipStream_t aux[TGMS_AUX_STREAMS] = {};
@@ -97,6 +107,32 @@ tgms_status ensure_ws(tgms_handle* h, size_t bytes) {
     }
     TGMS_HIP(h, hipMalloc(&h->d_ws, bytes));
     h->ws_cap = bytes;
+    return TGMS_OK;
+}
+
+// Order `stream` after every earlier user of the handle's device scratch.
+tgms_status scratch_acquire(tgms_handle* h, hipStream_t stream) {
+    if (h->scratch_pending) TGMS_HIP(h, hipStreamWaitEvent(stream, h->scratch_ev, 0));
+    return TGMS_OK;
+}
+
+// The work just enqueued on `stream` is the scratch's latest user.
+tgms_status scratch_release(tgms_handle* h, hipStream_t stream) {
+    TGMS_HIP(h, hipEventRecord(h->scratch_ev, stream));
+    h->scratch_pending = true;
+    return TGMS_OK;
+}
+
+tgms_status ensure_loop_ws(tgms_handle* h, size_t bytes) {
+    if (bytes <= h->loop_ws_cap) return TGMS_OK;
+    if (h->d_loop_ws) {
+        TGMS_HIP(h, hipDeviceSynchronize());
+        TGMS_HIP(h, hipFree(h->d_loop_ws));
+        h->d_loop_ws = nullptr;
+        h->loop_ws_cap = 0;
+    }
+    TGMS_HIP(h, hipMalloc(reinterpret_cast<void**>(&h->d_loop_ws), bytes));
+    h->loop_ws_cap = bytes;
     return TGMS_OK;
 }
 
@@ -457,7 +493,8 @@ tgms_status tgms_create(tgms_handle** out, int device) {
     h->device = device;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->perm_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->perm_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming) != hipSuccess) {
         delete h;
         return TGMS_ERR_DEVICE;
     }
@@ -475,6 +512,8 @@ void tgms_destroy(tgms_handle* h) {
     if (h->d_perm) (void)hipFree(h->d_perm);
     if (h->h_perm) (void)hipHostFree(h->h_perm);
     if (h->perm_ev) (void)hipEventDestroy(h->perm_ev);
+    if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
+    if (h->d_loop_ws) (void)hipFree(h->d_loop_ws);
     for (int j = 0; j < TGMS_AUX_STREAMS; ++j) {
         if (h->aux[j]) (void)hipStreamDestroy(h->aux[j]);
         if (h->join_ev[j]) (void)hipEventDestroy(h->join_ev[j]);
@@ -530,10 +569,13 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
     TGMS_HIP(h, hipMemcpyAsync(dT, seg_times, nT * 8, hipMemcpyHostToDevice, st));
     if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    s = scratch_acquire(h, st);
+    if (s != TGMS_OK) return s;
     Plan plan;
     s = make_plan(h, B, so, max_m_for(h), &plan, st);
     if (s != TGMS_OK) return s;
     s = dispatch(h, plan, B, dSo, dW, dT, dED, dC, dSt, st);
+    if (s == TGMS_OK) s = scratch_release(h, st);
     if (s != TGMS_OK) return s;
     TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     std::vector<int32_t> hst;
@@ -586,8 +628,10 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, cons
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (h->method == TGMS_METHOD_BAND_KKT) {
         tgms_status s = ensure_band(h, M, st);
+        if (s == TGMS_OK) s = scratch_acquire(h, st);
         if (s != TGMS_OK) return s;
         TGMS_HIP(h, tgms::launch_band_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, h->d_band, h->band_grid, st));
+        return scratch_release(h, st);
     } else if (h->method == TGMS_METHOD_REDUCED)
         TGMS_HIP(h, tgms::launch_reduced_uniform(M, B, dW, dT, dED, dC, dSt, st));
     else
@@ -605,10 +649,15 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
-    Plan plan;
-    s = make_plan(h, B, h_so, max_m_for(h), &plan, static_cast<hipStream_t>(stream));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    return dispatch(h, plan, B, d_so, dW, dT, dED, dC, dSt, static_cast<hipStream_t>(stream));
+    Plan plan;
+    s = make_plan(h, B, h_so, max_m_for(h), &plan, st);
+    if (s != TGMS_OK) return s;
+    s = dispatch(h, plan, B, d_so, dW, dT, dED, dC, dSt, st);
+    if (s != TGMS_OK) return s;
+    return scratch_release(h, st);
 }
 
 tgms_status tgms_refine_uniform_device(tgms_handle* h, int32_t B, int32_t M, const double* dW, const double* dT,
@@ -639,11 +688,15 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dT_out, d_cost);
-    Plan plan;
-    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, static_cast<hipStream_t>(stream));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    return dispatch_refine(h, plan, B, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt,
-                           static_cast<hipStream_t>(stream));
+    Plan plan;
+    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
+    if (s != TGMS_OK) return s;
+    s = dispatch_refine(h, plan, B, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt, st);
+    if (s != TGMS_OK) return s;
+    return scratch_release(h, st);
 }
 
 tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,
@@ -685,11 +738,14 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     TGMS_HIP(h, hipMemcpyAsync(dT[0], seg_times, S * 8, hipMemcpyHostToDevice, st));
     if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    s = scratch_acquire(h, st);
+    if (s != TGMS_OK) return s;
     Plan plan;
     s = make_plan(h, B, so, TGMS_MAX_SEGMENTS, &plan, st);
     if (s != TGMS_OK) return s;
     int cur = 0;
     s = refine_loop(h, plan, B, dSo, dW, dT, dED, k_T, eta, iters, coeffs ? dC : nullptr, dCost, dSt, st, &cur);
+    if (s == TGMS_OK) s = scratch_release(h, st);
     if (s != TGMS_OK) return s;
     if (coeffs) TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     TGMS_HIP(h, hipMemcpyAsync(seg_times, dT[cur], S * 8, hipMemcpyDeviceToHost, st));
@@ -722,9 +778,10 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t S = (size_t)h_so[B];
-    s = ensure_ws(h, align256(S * 8));
+    s = ensure_loop_ws(h, align256(S * 8));
+    if (s == TGMS_OK) s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    double* T[2] = {dT, static_cast<double*>(h->d_ws)};
+    double* T[2] = {dT, h->d_loop_ws};
     Plan plan;
     s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
     if (s != TGMS_OK) return s;
@@ -736,7 +793,10 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
         return TGMS_OK;
     };
     static const bool no_graph = std::getenv("TGMS_NO_GRAPH") != nullptr;
-    if (no_graph) return body(st);
+    if (no_graph) {
+        s = body(st);
+        return s != TGMS_OK ? s : scratch_release(h, st);
+    }
     // launch-bound (K x groups small kernels): capture once, replay while nothing changed
     tgms_handle::LoopKey key{B, iters, d_so, dW, dT, T[1], dED, dC, d_cost, dSt, h->d_perm, k_T, eta,
                              plan.counts, plan.starts, plan.uniform_m};
@@ -766,7 +826,7 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
         h->loop_key = key;
     }
     TGMS_HIP(h, hipGraphLaunch(h->loop_exec, st));
-    return TGMS_OK;
+    return scratch_release(h, st);
 }
 
 int64_t tgms_sample_count(double total_T, double dt) {

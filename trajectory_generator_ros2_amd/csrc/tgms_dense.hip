@@ -42,10 +42,7 @@ __device__ __forceinline__ double bcast(double v, int src) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-#ifndef TGMS_DENSE_NWV
-#define TGMS_DENSE_NWV 16
-#endif
-constexpr int NWV = TGMS_DENSE_NWV;
+constexpr int NWV = 16;  // wavefronts per trajectory
 #ifdef TGMS_DENSE_STAMPS  // diagnostic build: per-step phase timestamps of wave 0 in blocks < 64
 constexpr int DST_BLOCKS = 64, DST_STEPS = 160;
 __device__ unsigned long long g_dstamps[DST_BLOCKS * DST_STEPS * 4];
@@ -60,10 +57,7 @@ __device__ unsigned long long g_dstamps[DST_BLOCKS * DST_STEPS * 4];
     do {             \
     } while (0)
 #endif
-#ifndef TGMS_DENSE_DR
-#define TGMS_DENSE_DR 1
-#endif
-constexpr int DR = TGMS_DENSE_DR;  // rows per rank-1 update batch
+constexpr int DR = 1;  // rows per rank-1 update batch
 
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(W64 * NWV) void k_dense_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
@@ -223,15 +217,7 @@ __global__ __launch_bounds__(W64 * NWV) void k_dense_kkt(int32_t n_traj, const i
                 bidx = take ? oi[q] : bidx;
             }
         }
-#ifdef TGMS_DENSE_ABL_NOPIV  // ablation (timing only): no pivot search
-        best = 1.0;
-        bidx = k;
-#endif
-#ifdef TGMS_DENSE_ABL_NOSING  // ablation (timing only): never stop early
-        if (false) {
-#else
         if (!__builtin_amdgcn_readfirstlane(best > 0.0)) {  // identical in every wave
-#endif
             singular = true;
             break;
         }
@@ -299,11 +285,7 @@ __global__ __launch_bounds__(W64 * NWV) void k_dense_kkt(int32_t n_traj, const i
         int cidx = N;
         // rank-1 update, DR rows per batch so their LDS reads overlap; rows whose
         // multiplier is zero (most of them early on: the KKT is sparse) are skipped
-#ifdef TGMS_DENSE_ABL_NOUPD  // ablation (timing only): no rank-1 update
-        for (int pos0 = N; pos0 < N; pos0 += NWV * DR) {
-#else
         for (int pos0 = k + 1 + wave; pos0 < N; pos0 += NWV * DR) {
-#endif
             int ph[DR];
             double l[DR], a1[DR];
 #pragma unroll
@@ -348,11 +330,7 @@ __global__ __launch_bounds__(W64 * NWV) void k_dense_kkt(int32_t n_traj, const i
     DSTAMP(N, 0);
     if (wave != 0) return;
     // back substitution (column oriented, wave 0); x overwrites rhs
-#ifdef TGMS_DENSE_ABL_NOBS  // ablation (timing only)
-    if (false) {
-#else
     if (!singular) {
-#endif
         for (int k = N - 1; k >= 0; --k) {
             const int ks = k / W64, kl = k % W64;
             const double ipiv = ipiv_s[k];
@@ -420,14 +398,14 @@ hipError_t dense_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const 
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dense_kkt<M, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dense_kkt<M, true>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
+        TGMS_LAUNCH((k_dense_kkt<M, true>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
     } else {
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dense_kkt<M, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dense_kkt<M, false>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
+        TGMS_LAUNCH((k_dense_kkt<M, false>), dim3(n_traj), dim3(W64 * NWV), lds, stream, n_traj, ids, so, W, T, ED, C, status);
     }
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 }  // namespace

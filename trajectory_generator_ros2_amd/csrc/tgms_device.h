@@ -142,4 +142,24 @@ __device__ __forceinline__ double emit_segment(double T, double r, const double*
     return fin;
 }
 
+
+// Kernel launch that reports THIS launch's error: hipLaunchKernel returns it directly,
+// whereas hipLaunchKernelGGL + hipGetLastError() would also report (and clear) a
+// sticky error left by an unrelated earlier HIP call on the thread.
+template <class T>
+struct launch_arg {
+    using type = T;
+};
+template <class... KArgs>
+__host__ hipError_t launch_kernel(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t shmem, hipStream_t stream,
+                                  typename launch_arg<KArgs>::type... args) {
+    void* argv[] = {static_cast<void*>(&args)..., nullptr};
+    return hipLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, shmem, stream);
+}
+#define TGMS_LAUNCH(kernel, grid, block, shmem, stream, ...)                                       \
+    do {                                                                                         \
+        const hipError_t launch_e_ = ::tgms::launch_kernel(kernel, grid, block, shmem, stream, __VA_ARGS__); \
+        if (launch_e_ != hipSuccess) return launch_e_;                                           \
+    } while (0)
+
 }  // namespace tgms

@@ -36,24 +36,16 @@ namespace {
 
 // Waves per SIMD the register allocation must allow: two for the axis-sequential
 // solve while its state fits 256 registers without spilling (M <= 11), else one.
-#ifdef TGMS_MIN_WAVES
-#define TGMS_WAVES(M) TGMS_MIN_WAVES
-#else
 #define TGMS_WAVES(M) ((M) <= TGMS_TWO_WAVE_MAX_M ? 2 : 1)
-#endif
 
 // Scheduling fence between unrolled chain / emission steps.  The compiler-level
 // memory clobber also stops CSE of LDS reads across steps: re-reading LDS is far
 // cheaper than keeping values live.
-#ifndef TGMS_NO_SCHED_FENCE
 #define SCHED_FENCE()                      \
     do {                                   \
         asm volatile("" ::: "memory");     \
         __builtin_amdgcn_sched_barrier(0); \
     } while (0)
-#else
-#define SCHED_FENCE() ((void)0)
-#endif
 #ifdef TGMS_STAMPS  // diagnostic build: per-wave phase timestamps (s_memtime), lane 0
 __device__ unsigned long long g_stamps[8192 * 16];
 #define STAMP(i)                                                                              \
@@ -194,11 +186,7 @@ __device__ __forceinline__ OutCtx make_out(double* stage, const int64_t* base, d
 // enough.  (__syncthreads() would also fence global memory: vmcnt(0) on every
 // in-flight store.)
 __device__ __forceinline__ void wave_lds_sync() {
-#ifdef TGMS_LDS_NOWAIT  // experiment: rely on in-order DS execution within the wave
-    asm volatile("" ::: "memory");
-#else
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -222,11 +210,7 @@ __device__ __forceinline__ void stage_axis(const OutCtx& o, const double (&c)[8]
     const int offL = segL * 24 + a * 8, offR = segR * 24 + a * 8;
     auto put = [&](int q, const double2& v) {
         if (o.live[q] && (has_r || !o.rt[q])) {
-#ifdef TGMS_ABL_NOSTORE  // ablation: everything but the global stores
-            asm volatile("" ::"v"(v.x), "v"(v.y));
-#else
             *reinterpret_cast<double2*>(o.dst[q] + (o.rt[q] ? offR : offL)) = v;
-#endif
         }
     };
     put(0, v0);
@@ -300,7 +284,6 @@ __device__ __forceinline__ void stage_axis(const OutBuf& o, const double (&c)[8]
     };
     const double2 v0 = piece(0), v1 = piece(1), v2 = piece(2), v3 = piece(3);
     const uint32_t off = (has_r || !o.rt) ? voff : 0x80000000u;  // idle odd rows: out of range
-#ifndef TGMS_ABL_NOSTORE
     if (o.nt) {  // wave-uniform
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), o.rs[0], off, a * 64, TGMS_STORE_CPOL_NT);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), o.rs[1], off, a * 64, TGMS_STORE_CPOL_NT);
@@ -312,179 +295,11 @@ __device__ __forceinline__ void stage_axis(const OutBuf& o, const double (&c)[8]
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v2), o.rs[2], off, a * 64, TGMS_STORE_CPOL);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v3), o.rs[3], off, a * 64, TGMS_STORE_CPOL);
     }
-#else
-    asm volatile("" ::"v"(v0.x), "v"(v1.x), "v"(v2.x), "v"(v3.x), "v"(off));
-#endif
-}
-
-// Line-major output (uniform batches, even M; experiment, built with -DTGMS_LINES).
-// Beyond the Infinity Cache the HBM
-// write rate depends on whether the two 64-B halves of a 128-B line leave in the
-// same or in consecutive store instructions (scripts/storebench.hip, B = 524,288:
-// whole lines 5.5 TB/s; halves 4 instructions apart 3.9 TB/s; one axis per pass,
-// as the axis-sequential emission writes them, 3.4 TB/s).  A line of the
-// [traj][seg][axis][8] layout always holds two different axes, so the lines are
-// written after all three axes are solved: each lane computes the two rows of its
-// next line (its own rows in the virtual frame: the odd lane counts rows from the
-// trajectory's end), stages them as one 128-B LDS row, and every store
-// instruction writes 8 whole lines.  With 3M/2 lines per trajectory each lane owns
-// 3M/4 of them; for M = 2 mod 4 the middle line is shared (one row from each lane).
-template <int M>
-struct LineStage {
-    static constexpr int NLINE = 3 * M / 2;     // 128-B lines per trajectory
-    static constexpr int NFULL = (3 * M) / 4;   // whole lines per lane
-    static constexpr bool HALF = (3 * M) % 4 != 0;
-    alignas(16) double O[W64 * 16];             // one 128-B line per lane, 16-B chunks XOR-swizzled
-    RawIn<M> in;
-};
-
-struct OutLines {
-    double* stage;                  // LDS [W64][16] doubles
-    __amdgpu_buffer_rsrc_t rs;      // the wave's output block (range = its live trajectories)
-    uint32_t voff0;                 // byte offset of the lane's piece, line step 0, instruction 0
-    int32_t lstep;                  // +-128 B per line step
-    uint32_t voffh;                 // byte offset of the lane's piece of the middle line
-    uint32_t traj_b;                // bytes per trajectory
-    int lane;
-};
-
-template <int M>
-__device__ __forceinline__ OutLines make_out_lines(double* stage, double* C, int64_t b0, int nb, int lane) {
-    constexpr int TRAJ_B = M * 24 * 8;
-    constexpr int NLINE = LineStage<M>::NLINE;
-    OutLines o;
-    o.stage = stage;
-    o.lane = lane;
-    o.traj_b = TRAJ_B;
-    double* base = C + b0 * (M * 24);
-    const int block = nb * TRAJ_B;
-    o.rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, block, 0x00020000);
-    const bool side = (lane >> 3) & 1;  // the line was staged by an odd (right) lane
-    o.voff0 = (uint32_t)((lane >> 4) * TRAJ_B + (side ? (NLINE - 1) * 128 : 0) + (lane & 7) * 16);
-    o.lstep = side ? -128 : 128;
-    // middle line (M = 2 mod 4): instruction q covers trajectories 8q .. 8q+7
-    o.voffh = (uint32_t)((lane >> 3) * TRAJ_B + ((NLINE - 1) / 2) * 128 + (lane & 7) * 16);
-    return o;
-}
-
-__device__ __forceinline__ void stage_chunk(double* row, int c, int lane, double x, double y) {
-    *reinterpret_cast<double2*>(row + ((c ^ (lane & 7)) << 1)) = make_double2(x, y);
-}
-
-// Stage the lane's line (c0 = first half, c1 = second half in memory order) and
-// store 8 whole lines per instruction.
-__device__ __forceinline__ void store_line(const OutLines& o, const double (&c0)[8], const double (&c1)[8],
-                                           uint32_t voff) {
-    wave_lds_sync();  // previous readers are done with the stage
-    double* row = o.stage + o.lane * 16;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) stage_chunk(row, j, o.lane, c0[2 * j], c0[2 * j + 1]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) stage_chunk(row, 4 + j, o.lane, c1[2 * j], c1[2 * j + 1]);
-    wave_lds_sync();
-    double2 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int p = 8 * q + (o.lane >> 3), c = o.lane & 7;
-        v[q] = *reinterpret_cast<const double2*>(o.stage + p * 16 + ((c ^ (p & 7)) << 1));
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-#ifndef TGMS_ABL_NOSTORE
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[q]), o.rs, voff + q * 4 * o.traj_b, 0,
-                                               TGMS_STORE_CPOL);
-#else
-        asm volatile("" ::"v"(v[q].x), "v"(voff));
-#endif
-    }
-}
-
-// The middle line of M = 2 mod 4: the even lane's last row is its first half, the
-// odd lane's last row its second half; 32 lines, 4 instructions.
-__device__ __forceinline__ void store_half(const OutLines& o, const double (&c)[8]) {
-    wave_lds_sync();
-    double* row = o.stage + o.lane * 16;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) stage_chunk(row, j, o.lane, c[2 * j], c[2 * j + 1]);
-    wave_lds_sync();
-    double2 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int t = 8 * q + (o.lane >> 3), k = o.lane & 7, p = 2 * t + (k >> 2);
-        v[q] = *reinterpret_cast<const double2*>(o.stage + p * 16 + (((k & 3) ^ (p & 7)) << 1));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#ifndef TGMS_ABL_NOSTORE
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[q]), o.rs, o.voffh + q * 8 * o.traj_b, 0,
-                                               TGMS_STORE_CPOL);
-#else
-        asm volatile("" ::"v"(v[q].x));
-#endif
-    }
 }
 
 // Output address of emission step e for either output context.
 __device__ __forceinline__ uint32_t out_step(const OutBuf& o, int e) { return o.voff0 + e * o.estep; }
 __device__ __forceinline__ int out_step(const OutCtx&, int e) { return e; }
-
-// Coefficients of one physical segment (a4 layout [axis][8]) from its end data:
-// physical start knot (w0, g0) and end knot (w1, g1), g = (v, a, j) x axis.
-struct NoHook {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-
-// `hook(a)` runs after axis a is handed to the store path (software pipelining).
-template <class Hook = NoHook>
-__device__ __forceinline__ void emit_step(const OutCtx& o, double T, double r, const double* w0, const double* w1,
-                                          const double (&g0)[3][3], const double (&g1)[3][3], int segL, int segR,
-                                          bool has_r, Hook&& hook = Hook()) {
-    const double T2 = T * T, T3 = T2 * T;
-    double rp[8];
-    rpowers(r, rp);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double dw = w1[a] - w0[a];
-        const double v0 = g0[0][a], a0 = g0[1][a], j0 = g0[2][a];
-        const double v1 = g1[0][a], a1 = g1[1][a], j1 = g1[2][a];
-        const double h1 = T * v0, h2 = T2 * a0, h3 = T3 * j0;
-        const double h5 = T * v1, h6 = T2 * a1, h7 = T3 * j1;
-        const double d4 = 35.0 * dw - 20.0 * h1 - 5.0 * h2 - (2.0 / 3.0) * h3 - 15.0 * h5 + 2.5 * h6 -
-                          (1.0 / 6.0) * h7;
-        const double d5 = -84.0 * dw + 45.0 * h1 + 10.0 * h2 + h3 + 39.0 * h5 - 7.0 * h6 + 0.5 * h7;
-        const double d6 = 70.0 * dw - 36.0 * h1 - 7.5 * h2 - (2.0 / 3.0) * h3 - 34.0 * h5 + 6.5 * h6 -
-                          0.5 * h7;
-        const double d7 = -20.0 * dw + 10.0 * h1 + 2.0 * h2 + (1.0 / 6.0) * h3 + 10.0 * h5 - 2.0 * h6 +
-                          (1.0 / 6.0) * h7;
-        const double c[8] = {w0[a], v0, 0.5 * a0, j0 * (1.0 / 6.0), d4 * rp[4], d5 * rp[5], d6 * rp[6], d7 * rp[7]};
-        stage_axis(o, c, a, segL, segR, has_r);
-        hook(a);
-    }
-}
-
-// Emit virtual segment e (virtual knots e .. e+1, derivatives xs / xe).  The even
-// lane's virtual segment e is physical segment e; the odd lane's is physical
-// segment M-1-e traversed backwards (physical start = virtual knot e+1, with P).
-template <int M, class Hook = NoHook>
-__device__ __forceinline__ void emit_virtual(const OutCtx& o, const LaneView& L, bool right, int e,
-                                             const double (&xs)[3][3], const double (&xe)[3][3], bool has_r,
-                                             Hook&& hook = Hook()) {
-    const double sg = right ? -1.0 : 1.0;
-    double g0[3][3], g1[3][3], w0[3], w1[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double ws = L.w(e, a), we = L.w(e + 1, a);
-        w0[a] = right ? we : ws;
-        w1[a] = right ? ws : we;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const double f = (d == 1) ? 1.0 : sg;
-            g0[d][a] = right ? f * xe[d][a] : xs[d][a];
-            g1[d][a] = right ? f * xs[d][a] : xe[d][a];
-        }
-    }
-    emit_step(o, L.t(e), L.r(e), w0, w1, g0, g1, e, M - 1 - e, has_r, hook);
-}
 
 // ---------------------------------------------------------------------------
 // Block algebra.
@@ -567,270 +382,14 @@ __device__ __forceinline__ void coupling(const double (&p)[8], double (&B)[3][3]
 }
 
 // ---------------------------------------------------------------------------
-// One trajectory on a lane pair, as explicit phases over a PairState so that two
-// groups can be software-pipelined in one wavefront (k_reduced_pipe): the chain of
-// the next group runs between the emission steps of the current one.
-// Invalid trajectories were replaced by an all-zero, unit-time one during staging,
-// so they come out as exact zeros.
+// One trajectory on a lane pair.  Invalid trajectories were replaced by an
+// all-zero, unit-time one during staging, so they come out as exact zeros.
 template <int M>
 struct Chain {
     static constexpr int c = (M - 1) / 2;  // even chain: knots 1..c, odd chain: M-1..c+1
     static constexpr int nL = c, nR = M - 1 - c, NS = nR;
     static constexpr int NE = nL + 1;      // emission steps (even lane: nL+1 segments, odd: nR)
 };
-
-template <int M>
-struct PairState {
-    Ldl3 F[Chain<M>::NS];
-    double Y[Chain<M>::NS + 1][3][3];  // chain right-hand sides, then knot derivatives
-    double u0[3][3], uM[3][3];         // virtual-frame end derivatives [derivative][axis]
-    double pp[8];                      // powers of r of the segment left of the next knot
-    Sym3 Dl;                           // last pivot block of this lane's chain
-    double fin;                        // sum of the solved knot derivatives (finiteness)
-    bool spd;
-};
-
-template <int M, bool HAS_ED>
-__device__ __forceinline__ void ps_init(PairState<M>& S, const LaneView& L, bool right, bool valid,
-                                        const double* __restrict__ ed) {
-    // even lane (u0, uM); odd lane (P uM, P u0)
-    const double sg = right ? -1.0 : 1.0;
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
-            const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
-            const double f = (d == 1) ? 1.0 : sg;
-            S.u0[d][a] = right ? f * s1 : s0;
-            S.uM[d][a] = right ? f * s0 : s1;
-        }
-    S.spd = true;
-    S.fin = 0.0;
-    if constexpr (M >= 3) rpowers(L.r(0), S.pp);
-}
-
-// Elimination step s (virtual knot k = s+1) of the lane's chain, in three parts
-// so that it can be spread between the three axes of an emission step:
-//   0: diagonal block and right-hand side of knot k
-//   1: right-hand side update with the previous knot's solve
-//   2: Schur update of the diagonal block and its LDL^T
-struct ChainTmp {
-    Sym3 D;
-    double y[3][3];
-    double pn[8];
-};
-
-template <int M, bool HAS_ED>
-__device__ __forceinline__ void ps_chain_part(PairState<M>& S, ChainTmp& X, const LaneView& L, bool right, int s,
-                                              int part) {
-    using CH = Chain<M>;
-    const int k = s + 1;
-    if (part == 0) {
-        rpowers(L.r(k), X.pn);
-        X.D = knot_diag(S.pp, X.pn);
-        knot_rhs<HAS_ED>(L, k, S.pp, X.pn, S.u0, X.y);
-    } else if (part == 1) {
-        if (s >= 1) {
-            double B[3][3];
-            coupling(S.pp, B);  // H_{k-1, k}
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double v0, v1, v2;
-                ldl3_solve(S.F[s - 1], S.Y[s - 1][0][a], S.Y[s - 1][1][a], S.Y[s - 1][2][a], v0, v1, v2);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) X.y[d][a] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
-            }
-        }
-    } else {
-        const int nl = right ? CH::nR : CH::nL;
-        Sym3 D = X.D;
-        if (s >= 1) {
-            double B[3][3], Wc[3][3];
-            coupling(S.pp, B);
-#pragma unroll
-            for (int e = 0; e < 3; ++e)
-                ldl3_solve(S.F[s - 1], B[0][e], B[1][e], B[2][e], Wc[0][e], Wc[1][e], Wc[2][e]);
-            sym_sub_btw(D, B, Wc);
-        }
-        bool ok;
-        S.F[s] = ldl3s(D, ok);
-        S.spd = S.spd && (ok || s >= nl);
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-#pragma unroll
-            for (int a = 0; a < 3; ++a) S.Y[s][d][a] = X.y[d][a];
-        if (s == CH::nL - 1) S.Dl = D;
-        if (CH::nR > CH::nL && s == CH::nR - 1) {
-            S.Dl.a00 = right ? D.a00 : S.Dl.a00;
-            S.Dl.a01 = right ? D.a01 : S.Dl.a01;
-            S.Dl.a02 = right ? D.a02 : S.Dl.a02;
-            S.Dl.a11 = right ? D.a11 : S.Dl.a11;
-            S.Dl.a12 = right ? D.a12 : S.Dl.a12;
-            S.Dl.a22 = right ? D.a22 : S.Dl.a22;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) S.pp[q] = X.pn[q];
-    }
-}
-
-template <int M, bool HAS_ED>
-__device__ __forceinline__ void ps_chain_step(PairState<M>& S, const LaneView& L, bool right, int s) {
-    ChainTmp X;
-    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 0);
-    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 1);
-    ps_chain_part<M, HAS_ED>(S, X, L, right, s, 2);
-}
-
-// Interface (physical knots c and c+1) and back substitution: afterwards Y[0..NS]
-// hold the knot derivatives of virtual knots 1..NS+1 (Y[nl] = the other lane's
-// interface knot).
-template <int M>
-__device__ __forceinline__ void ps_finish(PairState<M>& S, const LaneView& L, bool right) {
-    using CH = Chain<M>;
-    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS;
-    const int nl = right ? nR : nL;
-    const double sg = right ? -1.0 : 1.0;
-    MARK(interface);
-    STAMP(2);
-    SCHED_FENCE();
-    // Each lane maps its last pivot block / right-hand side to the physical frame
-    // (P flips exactly), the even and odd lane broadcast theirs, and both lanes
-    // solve the same 6x6 system with bit-identical operations: x_c by the Schur
-    // complement onto knot c, then x_{c+1} back-solved from it.  (Two independent
-    // Schur solves leave x_c / x_{c+1} mutually inconsistent: ~70x less accurate.)
-    double xm[3][3];
-    {
-        Sym3 DL, DR;
-        {
-            const double p01 = sg * S.Dl.a01, p12 = sg * S.Dl.a12;
-            DL = Sym3{pair_even(S.Dl.a00), pair_even(p01), pair_even(S.Dl.a02),
-                      pair_even(S.Dl.a11), pair_even(p12), pair_even(S.Dl.a22)};
-            DR = Sym3{pair_odd(S.Dl.a00), pair_odd(p01), pair_odd(S.Dl.a02),
-                      pair_odd(S.Dl.a11), pair_odd(p12), pair_odd(S.Dl.a22)};
-        }
-        double Cc[3][3];  // H_{c, c+1}: physical segment c = virtual segment nl on both lanes
-        {
-            double pc[8];
-            rpowers(L.r(nl), pc);
-            coupling(pc, Cc);
-        }
-        bool ok1, ok2;
-        const Ldl3 FR = ldl3s(DR, ok1);
-        {
-            double Wm[3][3];
-#pragma unroll
-            for (int e = 0; e < 3; ++e) ldl3_solve(FR, Cc[e][0], Cc[e][1], Cc[e][2], Wm[0][e], Wm[1][e], Wm[2][e]);
-            DL.a00 -= Cc[0][0] * Wm[0][0] + Cc[0][1] * Wm[1][0] + Cc[0][2] * Wm[2][0];
-            DL.a01 -= Cc[0][0] * Wm[0][1] + Cc[0][1] * Wm[1][1] + Cc[0][2] * Wm[2][1];
-            DL.a02 -= Cc[0][0] * Wm[0][2] + Cc[0][1] * Wm[1][2] + Cc[0][2] * Wm[2][2];
-            DL.a11 -= Cc[1][0] * Wm[0][1] + Cc[1][1] * Wm[1][1] + Cc[1][2] * Wm[2][1];
-            DL.a12 -= Cc[1][0] * Wm[0][2] + Cc[1][1] * Wm[1][2] + Cc[1][2] * Wm[2][2];
-            DL.a22 -= Cc[2][0] * Wm[0][2] + Cc[2][1] * Wm[1][2] + Cc[2][2] * Wm[2][2];
-        }
-        const Ldl3 FS = ldl3s(DL, ok2);
-        S.spd = S.spd && ok1 && ok2;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            double yL[3], yR[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                // this lane's last chain right-hand side Y[nl-1], in the physical frame
-                const double yv = (nR > nL) ? (right ? S.Y[NS - 1][d][a] : S.Y[nL - 1][d][a]) : S.Y[nL - 1][d][a];
-                const double yp = (d == 1) ? yv : sg * yv;
-                yL[d] = pair_even(yp);
-                yR[d] = pair_odd(yp);
-            }
-            double g0, g1, g2;
-            ldl3_solve(FR, yR[0], yR[1], yR[2], g0, g1, g2);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
-            double xc0, xc1, xc2, x10, x11, x12;
-            ldl3_solve(FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
-            const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
-            const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
-            const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
-            ldl3_solve(FR, b0, b1, b2, x10, x11, x12);
-            // own / other interface knot in the lane's virtual frame
-            xm[0][a] = right ? -x10 : xc0;
-            xm[1][a] = right ? x11 : xc1;
-            xm[2][a] = right ? -x12 : xc2;
-            const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
-            if (nR > nL) {  // the other knot goes to slot nl: nL (even) / nR (odd)
-                S.Y[nL][0][a] = right ? S.Y[nL][0][a] : o0;
-                S.Y[nL][1][a] = right ? S.Y[nL][1][a] : o1;
-                S.Y[nL][2][a] = right ? S.Y[nL][2][a] : o2;
-                S.Y[nR][0][a] = right ? o0 : S.Y[nR][0][a];
-                S.Y[nR][1][a] = right ? o1 : S.Y[nR][1][a];
-                S.Y[nR][2][a] = right ? o2 : S.Y[nR][2][a];
-            } else {
-                S.Y[nL][0][a] = o0;
-                S.Y[nL][1][a] = o1;
-                S.Y[nL][2][a] = o2;
-            }
-            S.fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
-        }
-    }
-    MARK(backsub);
-    STAMP(3);
-    // ---- back substitution along the virtual chain: x_s = F_s^{-1}(y_s - C_{s+1} x_{s+1}) ----
-#pragma unroll
-    for (int s = NS - 1; s >= 0; --s) {
-        SCHED_FENCE();
-        const bool at_end = (s == nl - 1);
-        const bool inside = (s < nl - 1);
-        if (s + 1 < NS) {
-            double B[3][3];
-            {
-                double pb[8];
-                rpowers(L.r(s + 1), pb);
-                coupling(pb, B);  // H_{s+1, s+2} (virtual knots)
-            }
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double b[3], x0, x1, x2;
-#pragma unroll
-                for (int d = 0; d < 3; ++d)
-                    b[d] = S.Y[s][d][a] - (B[d][0] * S.Y[s + 1][0][a] + B[d][1] * S.Y[s + 1][1][a] + B[d][2] * S.Y[s + 1][2][a]);
-                ldl3_solve(S.F[s], b[0], b[1], b[2], x0, x1, x2);
-                S.Y[s][0][a] = at_end ? xm[0][a] : (inside ? x0 : S.Y[s][0][a]);
-                S.Y[s][1][a] = at_end ? xm[1][a] : (inside ? x1 : S.Y[s][1][a]);
-                S.Y[s][2][a] = at_end ? xm[2][a] : (inside ? x2 : S.Y[s][2][a]);
-                S.fin += inside ? (x0 + x1) + x2 : 0.0;
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) S.Y[s][d][a] = at_end ? xm[d][a] : S.Y[s][d][a];
-        }
-    }
-    MARK(emission);
-    STAMP(4);
-}
-
-// Emission step e: virtual segment e = virtual knots e..e+1.
-template <int M, class Hook = NoHook>
-__device__ __forceinline__ void ps_emit_step(const PairState<M>& S, const OutCtx& O, const LaneView& L, bool right,
-                                             int e, Hook&& hook = Hook()) {
-    using CH = Chain<M>;
-    double xs[3][3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) xs[d][a] = (e == 0) ? S.u0[d][a] : S.Y[e >= 1 ? e - 1 : 0][d][a];
-    emit_virtual<M>(O, L, right, e, xs, S.Y[e], e < CH::nR, hook);
-}
-
-template <int M>
-__device__ __forceinline__ int32_t ps_status(const PairState<M>& S, bool valid) {
-    const bool spd_pair = S.spd && (pair_swap(S.spd ? 1.0 : 0.0) != 0.0);
-    const double fin_pair = S.fin + pair_swap(S.fin);
-    if (!valid) return TGMS_ERR_INVALID_ARG;
-    if (!spd_pair) return TGMS_ERR_SINGULAR;
-    if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
-    return TGMS_OK;
-}
 
 // ---------------------------------------------------------------------------
 // Axis-sequential solve (default for M >= 3).  The 3x3 block factorisation is
@@ -1068,149 +627,6 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     const bool valid = get_valid(valid_src);
     MARK(ax_axisloop);
     double fin = 0.0;
-#ifdef TGMS_AX_PIPE  // experiment (measured ~2% slower: register pressure, no ILP gain)
-    // ---- software-pipelined axes: the back substitution + emission of axis a runs
-    // step by step beside the forward substitution of axis a+1 (independent chains;
-    // the live knot set stays ~NS+1 since one array drains as the other fills) ----
-    auto start_derivs = [&](int a, double (&u0)[3]) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
-            const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
-            u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
-        }
-    };
-    auto fwd_step = [&](int a, const double (&u0)[3], double (&Y)[NS + 1][3], double (&pp)[8], int s) {
-        const int k = s + 1;
-        double pn[8];
-        rpowers(L.r(k), pn);
-        double y[3];
-        knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
-        if (s >= 1) {
-            double B[3][3], v0, v1, v2;
-            coupling(pp, B);
-            ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
-        }
-#pragma unroll
-        for (int d = 0; d < 3; ++d) Y[s][d] = y[d];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) pp[q] = pn[q];
-    };
-    auto iface = [&](double (&Y)[NS + 1][3], double (&xm)[3]) {
-        double yL[3], yR[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const double yv = (nR > nL) ? (right ? Y[NS - 1][d] : Y[nL - 1][d]) : Y[nL - 1][d];
-            const double yp = (d == 1) ? yv : sg * yv;
-            yL[d] = pair_even(yp);
-            yR[d] = pair_odd(yp);
-        }
-        double Cc[3][3];
-        {
-            double pc[8];
-            rpowers(L.r(nl), pc);
-            coupling(pc, Cc);
-        }
-        double g0, g1, g2;
-        ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
-        double xc0, xc1, xc2, x10, x11, x12;
-        ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
-        const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
-        const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
-        const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
-        ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
-        xm[0] = right ? -x10 : xc0;
-        xm[1] = right ? x11 : xc1;
-        xm[2] = right ? -x12 : xc2;
-        const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
-        if (nR > nL) {
-            Y[nL][0] = right ? Y[nL][0] : o0;
-            Y[nL][1] = right ? Y[nL][1] : o1;
-            Y[nL][2] = right ? Y[nL][2] : o2;
-            Y[nR][0] = right ? o0 : Y[nR][0];
-            Y[nR][1] = right ? o1 : Y[nR][1];
-            Y[nR][2] = right ? o2 : Y[nR][2];
-        } else {
-            Y[nL][0] = o0;
-            Y[nL][1] = o1;
-            Y[nL][2] = o2;
-        }
-        fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
-    };
-    auto back_step = [&](int a, double (&Y)[NS + 1][3], const double (&xm)[3], int s) {
-        const bool at_end = (s == nl - 1);
-        const bool inside = (s < nl - 1);
-        if (s + 1 < NS) {
-            double B[3][3];
-            {
-                double pb[8];
-                rpowers(L.r(s + 1), pb);
-                coupling(pb, B);
-            }
-            double b[3], x0, x1, x2;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) b[d] = Y[s][d] - (B[d][0] * Y[s + 1][0] + B[d][1] * Y[s + 1][1] + B[d][2] * Y[s + 1][2]);
-            ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
-            Y[s][0] = at_end ? xm[0] : (inside ? x0 : Y[s][0]);
-            Y[s][1] = at_end ? xm[1] : (inside ? x1 : Y[s][1]);
-            Y[s][2] = at_end ? xm[2] : (inside ? x2 : Y[s][2]);
-            fin += inside ? (x0 + x1) + x2 : 0.0;
-        } else {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
-        }
-        if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR);
-    };
-    double YA[NS + 1][3], YB[NS + 1][3], xA[3], xB[3], uA[3], uB[3], pA[8], pB[8];
-    // axis 0: forward + interface
-    start_derivs(0, uA);
-    rpowers(L.r(0), pA);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        SCHED_FENCE();
-        fwd_step(0, uA, YA, pA, s);
-    }
-    SCHED_FENCE();
-    iface(YA, xA);
-    // axis 0 back/emit  ||  axis 1 forward
-    start_derivs(1, uB);
-    rpowers(L.r(0), pB);
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        SCHED_FENCE();
-        back_step(0, YA, xA, NS - 1 - k);
-        fwd_step(1, uB, YB, pB, k);
-    }
-    SCHED_FENCE();
-    emit_axis<M, Out>(O, L, right, 0, 0, uA, YA[0], 0 < nR);
-    SCHED_FENCE();
-    iface(YB, xB);
-    // axis 1 back/emit  ||  axis 2 forward
-    start_derivs(2, uA);
-    rpowers(L.r(0), pA);
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        SCHED_FENCE();
-        back_step(1, YB, xB, NS - 1 - k);
-        fwd_step(2, uA, YA, pA, k);
-    }
-    SCHED_FENCE();
-    emit_axis<M, Out>(O, L, right, 0, 1, uB, YB[0], 0 < nR);
-    SCHED_FENCE();
-    iface(YA, xA);
-    // axis 2 back/emit
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-        SCHED_FENCE();
-        back_step(2, YA, xA, NS - 1 - k);
-    }
-    SCHED_FENCE();
-    emit_axis<M, Out>(O, L, right, 0, 2, uA, YA[0], 0 < nR);
-#else
 #pragma unroll 1
     for (int a = 0; a < 3; ++a) {
         // virtual-frame start derivatives of this axis: even lane u0, odd lane P uM
@@ -1261,16 +677,12 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
                 yL[d] = pair_even(yp);
                 yR[d] = pair_odd(yp);
             }
-#ifdef TGMS_AX_KEEP_CC
-            const double(&Cc)[3][3] = Fa.Cc;
-#else  // recomputed per axis: 18 fewer live registers across the axis loop
-            double Cc[3][3];
+            double Cc[3][3];  // recomputed per axis: 18 fewer live registers across the axis loop
             {
                 double pc[8];
                 rpowers(L.r(nl), pc);
                 coupling(pc, Cc);
             }
-#endif
             double g0, g1, g2;
             ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
 #pragma unroll
@@ -1327,223 +739,13 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #pragma unroll
                 for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
             }
-#ifndef TGMS_AX_EMIT_AFTER
             if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR);
-#endif
         }
         MARK(ax_emit);
-#ifndef TGMS_AX_EMIT_AFTER
         SCHED_FENCE();
         emit_axis<M, Out>(O, L, right, 0, a, u0, Y[0], 0 < nR);
-#else
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            SCHED_FENCE();
-            double xs[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) xs[d] = (e == 0) ? u0[d] : Y[e >= 1 ? e - 1 : 0][d];
-            emit_axis<M, Out>(O, L, right, e, a, xs, Y[e], e < nR);
-        }
-#endif
     }
-#endif
     MARK(ax_end);
-    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
-    const double fin_pair = fin + pair_swap(fin);
-    if (!valid) return TGMS_ERR_INVALID_ARG;
-    if (!spd_pair) return TGMS_ERR_SINGULAR;
-    if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
-    return TGMS_OK;
-}
-
-// One axis of the axis-sequential solve without emission: forward substitution,
-// interface, back substitution.  On return Y[s] = virtual knot s+1 and u0 = the
-// virtual start derivatives (same arithmetic as pair_solve_ax's axis loop).
-template <int M, bool HAS_ED>
-__device__ __forceinline__ void axis_solve(const AxFactors<M>& Fa, const LaneView& L, bool right, int a, bool valid,
-                                           const double* __restrict__ ed, double (&u0)[3],
-                                           double (&Y)[Chain<M>::NS + 1][3], double& fin) {
-    using CH = Chain<M>;
-    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS;
-    const int nl = right ? nR : nL;
-    const double sg = right ? -1.0 : 1.0;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
-        const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
-        u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
-    }
-    {
-        double pp[8];
-        rpowers(L.r(0), pp);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            SCHED_FENCE();
-            const int k = s + 1;
-            double pn[8];
-            rpowers(L.r(k), pn);
-            double y[3];
-            knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
-            if (s >= 1) {
-                double B[3][3], v0, v1, v2;
-                coupling(pp, B);
-                ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
-            }
-#pragma unroll
-            for (int d = 0; d < 3; ++d) Y[s][d] = y[d];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
-        }
-    }
-    SCHED_FENCE();
-    double xm[3];
-    {
-        double yL[3], yR[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const double yv = (nR > nL) ? (right ? Y[NS - 1][d] : Y[nL - 1][d]) : Y[nL - 1][d];
-            const double yp = (d == 1) ? yv : sg * yv;
-            yL[d] = pair_even(yp);
-            yR[d] = pair_odd(yp);
-        }
-        double Cc[3][3];
-        {
-            double pc[8];
-            rpowers(L.r(nl), pc);
-            coupling(pc, Cc);
-        }
-        double g0, g1, g2;
-        ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
-        double xc0, xc1, xc2, x10, x11, x12;
-        ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
-        const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
-        const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
-        const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
-        ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
-        xm[0] = right ? -x10 : xc0;
-        xm[1] = right ? x11 : xc1;
-        xm[2] = right ? -x12 : xc2;
-        const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
-        if (nR > nL) {
-            Y[nL][0] = right ? Y[nL][0] : o0;
-            Y[nL][1] = right ? Y[nL][1] : o1;
-            Y[nL][2] = right ? Y[nL][2] : o2;
-            Y[nR][0] = right ? o0 : Y[nR][0];
-            Y[nR][1] = right ? o1 : Y[nR][1];
-            Y[nR][2] = right ? o2 : Y[nR][2];
-        } else {
-            Y[nL][0] = o0;
-            Y[nL][1] = o1;
-            Y[nL][2] = o2;
-        }
-        fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
-    }
-#pragma unroll
-    for (int s = NS - 1; s >= 0; --s) {
-        SCHED_FENCE();
-        const bool at_end = (s == nl - 1);
-        const bool inside = (s < nl - 1);
-        if (s + 1 < NS) {
-            double B[3][3];
-            {
-                double pb[8];
-                rpowers(L.r(s + 1), pb);
-                coupling(pb, B);
-            }
-            double b[3], x0, x1, x2;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) b[d] = Y[s][d] - (B[d][0] * Y[s + 1][0] + B[d][1] * Y[s + 1][1] + B[d][2] * Y[s + 1][2]);
-            ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
-            Y[s][0] = at_end ? xm[0] : (inside ? x0 : Y[s][0]);
-            Y[s][1] = at_end ? xm[1] : (inside ? x1 : Y[s][1]);
-            Y[s][2] = at_end ? xm[2] : (inside ? x2 : Y[s][2]);
-            fin += inside ? (x0 + x1) + x2 : 0.0;
-        } else {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
-        }
-    }
-}
-
-// Coefficients of the lane's virtual row q (0 .. 3M/2-1): virtual segment q / 3,
-// axis q % 3 on the even lane and 2 - q % 3 on the odd lane, whose rows run from
-// the trajectory's end (physical row 3M-1-q).
-template <int M>
-__device__ __forceinline__ void lane_row(const LaneView& L, bool right, int q, const double (&u0)[3][3],
-                                         const double (&Y)[3][Chain<M>::NS + 1][3], double (&c)[8]) {
-    const int e = q / 3, slot = q % 3;
-    double xs[3], xe[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const double s_a = (e == 0) ? u0[slot][d] : Y[slot][e >= 1 ? e - 1 : 0][d];
-        const double s_b = (e == 0) ? u0[2 - slot][d] : Y[2 - slot][e >= 1 ? e - 1 : 0][d];
-        xs[d] = right ? s_b : s_a;
-        xe[d] = right ? Y[2 - slot][e][d] : Y[slot][e][d];
-    }
-    row_coeffs(L, right, e, right ? 2 - slot : slot, xs, xe, c);
-}
-
-// Axis-sequential solve of all three axes, then line-major emission (even M).
-template <int M, bool HAS_ED, class V>
-__device__ __forceinline__ int32_t pair_solve_lines(const LaneView& L, bool right, V&& valid_src,
-                                                    const double* __restrict__ ed, const OutLines& O) {
-    using CH = Chain<M>;
-    using LS = LineStage<M>;
-    static_assert(M % 2 == 0 && M >= 4, "line-major emission needs even M >= 4");
-    static_assert(CH::NE == CH::NS && CH::nR == CH::NS, "even M: both lanes emit NS segments");
-    constexpr int NS = CH::NS;
-    AxFactors<M> Fa;
-    ax_factor<M>(Fa, L, right);
-    const bool valid = get_valid(valid_src);
-    double fin = 0.0;
-    double u0[3][3];
-    double Y[3][NS + 1][3];
-    axis_solve<M, HAS_ED>(Fa, L, right, 0, valid, ed, u0[0], Y[0], fin);
-    // the line stage is idle until the emission: park axis 0's knot data there
-    // ([value][lane], conflict-free) while the other two axes are solved (the
-    // two-wave builds; one wave per SIMD has the registers)
-    constexpr bool PARK = NS * 3 <= 16 && TGMS_WAVES(M) == 2;
-    SCHED_FENCE();
-    if constexpr (PARK) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int d = 0; d < 3; ++d) O.stage[(s * 3 + d) * W64 + O.lane] = Y[0][s][d];
-    }
-    axis_solve<M, HAS_ED>(Fa, L, right, 1, valid, ed, u0[1], Y[1], fin);
-    axis_solve<M, HAS_ED>(Fa, L, right, 2, valid, ed, u0[2], Y[2], fin);
-    SCHED_FENCE();
-    if constexpr (PARK) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int d = 0; d < 3; ++d) Y[0][s][d] = O.stage[(s * 3 + d) * W64 + O.lane];
-    }
-    MARK(lines);
-#pragma unroll
-    for (int k = 0; k < LS::NFULL; ++k) {
-        SCHED_FENCE();
-        double r0[8], r1[8];
-        lane_row<M>(L, right, 2 * k, u0, Y, r0);
-        lane_row<M>(L, right, 2 * k + 1, u0, Y, r1);
-        double h0[8], h1[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            h0[j] = right ? r1[j] : r0[j];
-            h1[j] = right ? r0[j] : r1[j];
-        }
-        store_line(O, h0, h1, O.voff0 + k * O.lstep);
-    }
-    if constexpr (LS::HALF) {
-        SCHED_FENCE();
-        double r0[8];
-        lane_row<M>(L, right, 2 * LS::NFULL, u0, Y, r0);
-        store_half(O, r0);
-    }
     const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
@@ -1616,38 +818,8 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
         if (!spd_pair) return TGMS_ERR_SINGULAR;
         if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
         return TGMS_OK;
-    } else if constexpr (!__is_same(Out, OutCtx)) {
-        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid_src, ed, O);
     } else {
-#ifndef TGMS_JOINT_AXES
-        return pair_solve_ax<M, HAS_ED, OutCtx>(L, right, valid_src, ed, O);
-#endif
-        const bool valid = get_valid(valid_src);
-        using CH = Chain<M>;
-        PairState<M> S;
-        ps_init<M, HAS_ED>(S, L, right, valid, ed);
-#ifdef TGMS_ABL_NOCOMPUTE  // ablation: staging + emission only, knot derivatives = 0
-#pragma unroll
-        for (int s = 0; s <= CH::NS; ++s)
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) S.Y[s][d][a] = 0.0;
-#else
-        MARK(chain);
-#pragma unroll
-        for (int s = 0; s < CH::NS; ++s) {
-            SCHED_FENCE();
-            ps_chain_step<M, HAS_ED>(S, L, right, s);
-        }
-        ps_finish<M>(S, L, right);
-#endif
-#pragma unroll
-        for (int e = 0; e < CH::NE; ++e) {
-            SCHED_FENCE();
-            ps_emit_step<M>(S, O, L, right, e);
-        }
-        return ps_status<M>(S, valid);
+        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid_src, ed, O);
     }
 }
 
@@ -1679,161 +851,6 @@ __device__ __forceinline__ void sanitize(In<M>& sm, int lane) {
     }
 }
 
-// A uniform group's inputs in registers: its 32 trajectories are one contiguous
-// HBM block, read with 16-B loads across the wave.  The loads are unconditional
-// (no divergent paths, so their registers can stay in flight across other work):
-// indices are clamped into the array, and the one double a clamped pair can miss
-// (the array's last, when its length is odd) is read separately.
-template <int M>
-struct Loads {
-    static constexpr int NW = (M + 1) * 3;
-    static constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 loads per lane, waypoints
-    static constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 loads per lane, times
-    double2 wv[NW2], tv[NT2];
-    double wlast, tlast;
-};
-
-template <int M>
-__device__ __forceinline__ void issue_loads(Loads<M>& R, const double* __restrict__ W, const double* __restrict__ T,
-                                            int32_t B, int64_t b0, int lane) {
-#ifndef TGMS_ABL_NOLOAD  // ablation: skip the input loads
-    using LD = Loads<M>;
-    const int64_t nW = (int64_t)B * LD::NW, nT = (int64_t)B * M;  // doubles in the arrays
-    const int64_t jW = b0 * LD::NW / 2, jT = b0 * M / 2;          // first double2 of the group (b0 even)
-    const double2* W2 = reinterpret_cast<const double2*>(W);
-    const double2* T2 = reinterpret_cast<const double2*>(T);
-#pragma unroll
-    for (int i = 0; i < LD::NW2; ++i) {
-        const int64_t j = jW + lane + W64 * i;
-        R.wv[i] = W2[j < nW / 2 ? j : nW / 2 - 1];
-    }
-#pragma unroll
-    for (int i = 0; i < LD::NT2; ++i) {
-        const int64_t j = jT + lane + W64 * i;
-        R.tv[i] = T2[j < nT / 2 ? j : nT / 2 - 1];
-    }
-    R.wlast = W[nW - 1];
-    R.tlast = T[nT - 1];
-#endif
-}
-
-// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left open (gfx9 encoding), as a real
-// waitcnt instruction the compiler's wait bookkeeping sees.
-constexpr unsigned VMCNT0 = 0x0F70;
-
-// The same loads as issue_loads, but straight into LDS (LDS-DMA, no VGPRs): the
-// wave's raw 16-B pieces land lane-linearly over dst's W/T/R arrays (dst is not in
-// use yet); raw_to_regs reads them back in issue_loads' register order.
-// Issued from inline asm: the compiler does not track these loads, so it cannot
-// insert conservative vmcnt(0) waits before unrelated LDS accesses; the matching
-// wait is the explicit one at the top of raw_to_regs (asm "memory" clobbers keep
-// every LDS access to dst on the right side of both).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-template <int M>
-__device__ __forceinline__ void issue_loads_lds(In<M>& dst, const double* __restrict__ W,
-                                                const double* __restrict__ T, int32_t B, int64_t b0, int lane) {
-    using LD = Loads<M>;
-    static_assert((LD::NW2 + LD::NT2) * W64 * 16 <= sizeof(double) * ((M + 1) * 3 + 2 * M) * PSTRIDE,
-                  "raw pieces must fit over W, T and R");
-    typedef __attribute__((address_space(3))) char lds_char;
-    const uint32_t raw = (uint32_t)(uintptr_t)(lds_char*)(dst.W);  // LDS byte address
-    const int64_t nW = (int64_t)B * LD::NW, nT = (int64_t)B * M;
-    const int64_t jW = b0 * LD::NW / 2, jT = b0 * M / 2;
-    const double2* W2 = reinterpret_cast<const double2*>(W);
-    const double2* T2 = reinterpret_cast<const double2*>(T);
-#pragma unroll
-    for (int i = 0; i < LD::NW2; ++i) {
-        const int64_t j = jW + lane + W64 * i;
-        glds16(W2 + (j < nW / 2 ? j : nW / 2 - 1), raw + i * W64 * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < LD::NT2; ++i) {
-        const int64_t j = jT + lane + W64 * i;
-        glds16(T2 + (j < nT / 2 ? j : nT / 2 - 1), raw + (LD::NW2 + i) * W64 * 16);
-    }
-}
-
-template <int M>
-__device__ __forceinline__ void raw_to_regs(const In<M>& src, Loads<M>& R, int lane) {
-    using LD = Loads<M>;
-    const double2* raw = reinterpret_cast<const double2*>(src.W);
-    // the LDS-DMA pieces have landed (an asm wait: the compiler does not know about
-    // the asm loads and would drop a builtin wait as redundant)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < LD::NW2; ++i) R.wv[i] = raw[i * W64 + lane];
-#pragma unroll
-    for (int i = 0; i < LD::NT2; ++i) R.tv[i] = raw[(LD::NW2 + i) * W64 + lane];
-    wave_lds_sync();  // every piece read before staging overwrites them
-}
-
-// Transpose a group's registers into LDS [field][trajectory] and flag invalid
-// trajectories (non-finite waypoint, T <= 0 or non-finite): only a wave that sees
-// one takes the LDS-atomic path and sanitises.
-template <int M>
-__device__ __forceinline__ void stage_loads(In<M>& sm, const Loads<M>& R, int32_t B, int64_t b0, int nb, int lane) {
-    using LD = Loads<M>;
-    const int nw = nb * LD::NW, nt = nb * M;  // doubles present in this group
-    const int64_t oddW = ((int64_t)B * LD::NW) & 1 ? (int64_t)B * LD::NW - 1 - b0 * LD::NW : -1;  // group-local
-    const int64_t oddT = ((int64_t)B * M) & 1 ? (int64_t)B * M - 1 - b0 * M : -1;
-    if (lane < TPW) sm.base[lane] = (b0 + lane) * (24 * M);
-    bool bad = false;
-#ifndef TGMS_ABL_NOLOAD
-    auto put_w = [&](int e, double v) {
-        if (e < nw) {
-            v = (e == oddW) ? R.wlast : v;
-            const int t = e / LD::NW, q = e - t * LD::NW;
-            sm.W[q * PSTRIDE + t] = v;
-            bad = bad || !finite(v);
-        }
-    };
-    auto put_t = [&](int e, double v) {
-        if (e < nt) {
-            v = (e == oddT) ? R.tlast : v;
-            const int t = e / M, q = e - t * M;
-            sm.T[q * PSTRIDE + t] = v;
-            sm.R[q * PSTRIDE + t] = fast_rcp(v);
-            bad = bad || !finite_pos(v);
-        }
-    };
-#pragma unroll
-    for (int i = 0; i < LD::NW2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        put_w(e, R.wv[i].x);
-        put_w(e + 1, R.wv[i].y);
-    }
-#pragma unroll
-    for (int i = 0; i < LD::NT2; ++i) {
-        const int e = 2 * (lane + W64 * i);
-        put_t(e, R.tv[i].x);
-        put_t(e + 1, R.tv[i].y);
-    }
-#endif
-    if (lane < TPW) sm.bad[lane] = 0;
-    wave_lds_sync();
-    if (__builtin_amdgcn_ballot_w64(bad) != 0) {  // rare: find the trajectories and sanitise them
-        for (int e = lane; e < nw; e += W64) {
-            const int t = e / LD::NW, q = e - t * LD::NW;
-            if (!finite(sm.W[q * PSTRIDE + t])) atomicOr(&sm.bad[t], 1);
-        }
-        for (int e = lane; e < nt; e += W64) {
-            const int t = e / M, q = e - t * M;
-            if (!finite_pos(sm.T[q * PSTRIDE + t])) atomicOr(&sm.bad[t], 1);
-        }
-        wave_lds_sync();
-        sanitize(sm, lane);
-        wave_lds_sync();
-    }
-}
-
 // Stage a uniform group into the raw layout: 16-B loads (indices clamped into the
 // arrays, so no lane branches), copied lane-linearly to LDS; 1/T computed in
 // registers.  The times are issued first and staged first, so the factorisation
@@ -1859,7 +876,6 @@ struct RawLoader {
         const int jmaxT = mT < (1 << 30) ? (int)mT : (1 << 30);
         const double2* gW = reinterpret_cast<const double2*>(W) + jW;
         const double2* gT = reinterpret_cast<const double2*>(T) + jT;
-#ifndef TGMS_ABL_NOLOAD
 #pragma unroll
         for (int i = 0; i < NT2; ++i) {
             const int j = lane + W64 * i;
@@ -1870,12 +886,6 @@ struct RawLoader {
             const int j = lane + W64 * i;
             wv[i] = gW[j < jmaxW ? j : jmaxW];
         }
-#else
-#pragma unroll
-        for (int i = 0; i < NT2; ++i) tv[i] = make_double2(1.0 + lane, 2.0);
-#pragma unroll
-        for (int i = 0; i < NW2; ++i) wv[i] = make_double2(lane, i);
-#endif
         nw = nb * NW;
         nt = nb * M;
         // an array of odd length: its last double is outside every clamped pair
@@ -1964,12 +974,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
                                                                         const double* __restrict__ ED,
                                                                         double* __restrict__ C,
                                                                         int32_t* __restrict__ status, int nt) {
-#ifdef TGMS_LINES  // experiment: line-major emission (see LineStage; slower at config 3)
-    constexpr bool LINES = (M % 2 == 0) && M >= 4;
-#else
-    constexpr bool LINES = false;
-#endif
-    __shared__ std::conditional_t<LINES, LineStage<M>, RawStage<M>> sm;
+    __shared__ RawStage<M> sm;
     STAMP_RT(6);
     STAMP(0);
     const int lane = threadIdx.x;
@@ -1991,129 +996,11 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
         return !any_bad || sm.in.bad[slot] == 0;
     };
     const LaneView L = make_view_raw<M>(sm.in, slot, right);
-    int32_t st;
-    if constexpr (LINES) {
-        const OutLines O = make_out_lines<M>(sm.O, C, b0, nb, lane);
-        st = pair_solve_lines<M, HAS_ED>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
-    } else {
-        const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane, nt != 0);
-        st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
-    }
+    const OutBuf O = make_out_buf<M>(sm.O, C, b0, nb, lane, nt != 0);
+    const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
     STAMP(5);
     STAMP_RT(7);
     if (live && !right && status) status[b] = st;
-}
-
-// Two groups per wavefront, software-pipelined: the second group's loads are in
-// flight during the first group's chain, and the second group's chain runs between
-// the first group's emission steps, so the coefficient stores of one group drain
-// while the other is being solved (one wave per SIMD cannot hide either otherwise).
-// Wave w solves groups w and w + gridDim.x.
-template <int M, bool HAS_ED>
-__global__ __launch_bounds__(64, 1) void k_reduced_pipe(int32_t B, const double* __restrict__ W,
-                                                         const double* __restrict__ T,
-                                                         const double* __restrict__ ED, double* __restrict__ C,
-                                                         int32_t* __restrict__ status) {
-    using CH = Chain<M>;
-    // separate LDS objects, so the compiler can tell B's in-flight LDS-DMA from
-    // every access to A's inputs and to the output stage (no false vmcnt waits)
-    __shared__ alignas(16) double stageO[W64 * OSTRIDE];
-    __shared__ In<M> inA;
-    __shared__ In<M> inB;
-    STAMP_RT(6);
-    STAMP(0);
-    const int lane = threadIdx.x;
-    const int slot = lane >> 1;
-    const bool right = lane & 1;
-    const int64_t ngroups = ((int64_t)B + TPW - 1) / TPW;
-    const int64_t gA = blockIdx.x, gB = gA + gridDim.x;
-    const bool twoB = gB < ngroups;  // wave-uniform
-    const int64_t bA0 = gA * TPW, bB0 = gB * TPW;
-    const int nbA = (int)((B - bA0) < TPW ? (B - bA0) : TPW);
-    const int nbB = twoB ? (int)((B - bB0) < TPW ? (B - bB0) : TPW) : 0;
-
-    Loads<M> RA, RB;
-    issue_loads<M>(RA, W, T, B, bA0, lane);
-    SCHED_FENCE();
-    stage_loads<M>(inA, RA, B, bA0, nbA, lane);
-    // retire every load of A (some are consumed on one path only), so no later
-    // register reuse makes the compiler wait for B's in-flight LDS-DMA
-    __builtin_amdgcn_s_waitcnt(VMCNT0);
-    SCHED_FENCE();
-    // B's inputs land in LDS while A is being solved
-    if (twoB) issue_loads_lds<M>(inB, W, T, B, bB0, lane);
-    RB.wlast = RA.wlast;  // array-wide values (the arrays' last doubles)
-    RB.tlast = RA.tlast;
-    STAMP(1);
-
-    // ---- group A: chain + interface + back substitution ----
-    const bool liveA = slot < nbA;
-    const int64_t bA = bA0 + slot;
-    const bool validA = inA.bad[slot] == 0;
-    const LaneView LA = make_view<M>(inA, slot, right);
-    PairState<M> SA;
-    ps_init<M, HAS_ED>(SA, LA, right, validA, (HAS_ED && liveA) ? ED + bA * 18 : ED);
-#pragma unroll
-    for (int s = 0; s < CH::NS; ++s) {
-        SCHED_FENCE();
-        ps_chain_step<M, HAS_ED>(SA, LA, right, s);
-    }
-    ps_finish<M>(SA, LA, right);
-    {
-        const int32_t st = ps_status<M>(SA, validA);
-        if (liveA && !right && status) status[bA] = st;
-    }
-    const OutCtx OA = make_out(stageO, inA.base, C, nbA, lane);
-
-    if (twoB) {
-        SCHED_FENCE();
-        raw_to_regs<M>(inB, RB, lane);
-        stage_loads<M>(inB, RB, B, bB0, nbB, lane);
-        const bool liveB = slot < nbB;
-        const int64_t bB = bB0 + slot;
-        const bool validB = inB.bad[slot] == 0;
-        const LaneView LB = make_view<M>(inB, slot, right);
-        PairState<M> SB;
-        ps_init<M, HAS_ED>(SB, LB, right, validB, (HAS_ED && liveB) ? ED + bB * 18 : ED);
-        // ---- emission of A interleaved with the chain of B ----
-#pragma unroll
-        for (int e = 0; e < CH::NE; ++e) {
-            SCHED_FENCE();
-#ifdef TGMS_PIPE_FINE  // one chain part after each axis of the emission step
-            ChainTmp X;
-            ps_emit_step<M>(SA, OA, LA, right, e, [&](int a) {
-                if (e < CH::NS) ps_chain_part<M, HAS_ED>(SB, X, LB, right, e, a);
-            });
-#else  // whole chain step after the emission step
-            ps_emit_step<M>(SA, OA, LA, right, e);
-            if (e < CH::NS) ps_chain_step<M, HAS_ED>(SB, LB, right, e);
-#endif
-        }
-#pragma unroll
-        for (int s = CH::NE; s < CH::NS; ++s) {
-            SCHED_FENCE();
-            ps_chain_step<M, HAS_ED>(SB, LB, right, s);
-        }
-        ps_finish<M>(SB, LB, right);
-        {
-            const int32_t st = ps_status<M>(SB, validB);
-            if (liveB && !right && status) status[bB] = st;
-        }
-        const OutCtx OB = make_out(stageO, inB.base, C, nbB, lane);
-#pragma unroll
-        for (int e = 0; e < CH::NE; ++e) {
-            SCHED_FENCE();
-            ps_emit_step<M>(SB, OB, LB, right, e);
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < CH::NE; ++e) {
-            SCHED_FENCE();
-            ps_emit_step<M>(SA, OA, LA, right, e);
-        }
-    }
-    STAMP(5);
-    STAMP_RT(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -2498,38 +1385,19 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(Group
     }
 }
 
-// The pipelined kernel needs both groups' inputs in LDS with 4 waves per CU
-// (one per SIMD): 160 KiB / 4.
-template <int M>
-constexpr bool use_pipe() {
-#ifndef TGMS_PIPE  // experiment (one wave per SIMD); the default is the 2-wave axis-sequential solve
-    return false;
-#else
-    return M >= 3 && sizeof(double) * W64 * OSTRIDE + 2 * sizeof(In<M>) <= 40 * 1024;
-#endif
-}
-
 template <int M>
 hipError_t uniform_M(int32_t B, const double* W, const double* T, const double* ED, double* C, int32_t* status,
                      hipStream_t stream) {
     const unsigned grid = (unsigned)((B + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
-    if constexpr (use_pipe<M>()) {
-        const unsigned g2 = (grid + 1) / 2;
-        if (ED)
-            hipLaunchKernelGGL((k_reduced_pipe<M, true>), dim3(g2), dim3(W64), 0, stream, B, W, T, ED, C, status);
-        else
-            hipLaunchKernelGGL((k_reduced_pipe<M, false>), dim3(g2), dim3(W64), 0, stream, B, W, T, ED, C, status);
-        return hipGetLastError();
-    }
     const int nt = (int64_t)B * M * 24 * 8 > kStreamingOutputBytes;
     if (ED)
-        hipLaunchKernelGGL((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
+        TGMS_LAUNCH((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
                            nt);
     else
-        hipLaunchKernelGGL((k_reduced_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
+        TGMS_LAUNCH((k_reduced_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
                            nt);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 template <int M>
@@ -2538,12 +1406,12 @@ hipError_t ragged_M(int32_t n, const int32_t* perm, const int32_t* so, const dou
     const unsigned grid = (unsigned)((n + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
     if (ED)
-        hipLaunchKernelGGL((k_reduced_ragged<M, true>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, C,
+        TGMS_LAUNCH((k_reduced_ragged<M, true>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, C,
                            status);
     else
-        hipLaunchKernelGGL((k_reduced_ragged<M, false>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, C,
+        TGMS_LAUNCH((k_reduced_ragged<M, false>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, C,
                            status);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 template <int M>
@@ -2552,12 +1420,12 @@ hipError_t refine_uniform_M(int32_t B, const double* W, const double* T, const d
     const unsigned grid = (unsigned)((B + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
     if (ED)
-        hipLaunchKernelGGL((k_refine_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta, Tout,
+        TGMS_LAUNCH((k_refine_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta, Tout,
                            cost, status);
     else
-        hipLaunchKernelGGL((k_refine_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta,
+        TGMS_LAUNCH((k_refine_uniform<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, kT, eta,
                            Tout, cost, status);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 template <int M>
@@ -2567,12 +1435,12 @@ hipError_t refine_ragged_M(int32_t n, const int32_t* perm, const int32_t* so, co
     const unsigned grid = (unsigned)((n + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
     if (ED)
-        hipLaunchKernelGGL((k_refine_ragged<M, true>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
+        TGMS_LAUNCH((k_refine_ragged<M, true>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
                            eta, Tout, cost, status);
     else
-        hipLaunchKernelGGL((k_refine_ragged<M, false>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
+        TGMS_LAUNCH((k_refine_ragged<M, false>), dim3(grid), dim3(W64), 0, stream, n, perm, so, W, T, ED, kT,
                            eta, Tout, cost, status);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 template <int MLO, int MHI>
@@ -2584,20 +1452,20 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
     if (grid == 0) return hipSuccess;
     if (refine) {
         if (ED)
-            hipLaunchKernelGGL((k_refine_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
+            TGMS_LAUNCH((k_refine_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
                                kT, eta, Tout, cost, status);
         else
-            hipLaunchKernelGGL((k_refine_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
+            TGMS_LAUNCH((k_refine_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
                                kT, eta, Tout, cost, status);
     } else {
         if (ED)
-            hipLaunchKernelGGL((k_reduced_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+            TGMS_LAUNCH((k_reduced_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
                                ED, C, status);
         else
-            hipLaunchKernelGGL((k_reduced_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+            TGMS_LAUNCH((k_reduced_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
                                ED, C, status);
     }
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 }  // namespace
@@ -2609,12 +1477,12 @@ hipError_t loop_multi_launch(const GroupTable& tab, const int32_t* so, const dou
     const unsigned grid = tab.ngroups ? (unsigned)tab.blk_end[tab.ngroups - 1] : 0u;
     if (grid == 0) return hipSuccess;
     if (ED)
-        hipLaunchKernelGGL((k_refine_loop_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
                            ED, kT, eta, iters, cost, C, status);
     else
-        hipLaunchKernelGGL((k_refine_loop_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
+        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
                            ED, kT, eta, iters, cost, C, status);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* so, const double* W, double* T,
@@ -2633,11 +1501,7 @@ hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, cons
     return multi_launch<TGMS_TWO_WAVE_MAX_M + 1, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
 }
 
-#ifdef TGMS_ONLY_M  // compile-only experiments: instantiate a single M
-#define TGMS_CASES(X) X(TGMS_ONLY_M)
-#else
 #define TGMS_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
-#endif
 
 hipError_t launch_reduced_uniform(int M, int32_t B, const double* W, const double* T, const double* ED,
                                   double* C, int32_t* status, hipStream_t stream) {

@@ -116,11 +116,7 @@ __global__ __launch_bounds__(W64 * SW) void k_sample(int32_t B, const int32_t* _
             // across the atan2 below, which keeps three waves per SIMD resident)
             double* so = stage[wave] + lane * G;
             double v[2], ac[2];
-#ifdef TGMS_SAMPLE_ABL_NOCOMPUTE  // ablation: store path only
-            if (false) {
-#else
             if (k < ns - 1) {
-#endif
                 const double t = (double)k * dt;
                 while (i + 1 < M && t_next <= t) {  // same test as the oracle's scan
                     ++i;
@@ -163,9 +159,7 @@ __global__ __launch_bounds__(W64 * SW) void k_sample(int32_t B, const int32_t* _
                     }
                 }
             }
-#ifndef TGMS_SAMPLE_ABL_NOCOMPUTE
             yaw_of(yaw_mode, yaw_const, v, ac, so[12], so[13]);
-#endif
             // 7 coalesced 16-B stores per lane of the wave's 64 staged samples
             __builtin_amdgcn_wave_barrier();
             const int64_t n2 = (ns - k0) * (G / 2);  // double2 of this chunk inside the trajectory
@@ -195,9 +189,9 @@ hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W,
     const int pieces = (int)std::min<int64_t>(4, std::max<int64_t>(1, (kItems + B - 1) / B));
     const int64_t items = (int64_t)B * pieces;
     const int64_t blocks = items < 65536 ? items : 65536;
-    hipLaunchKernelGGL(k_sample, dim3((unsigned)blocks), dim3(W64 * SW), 0, stream, B, seg_offsets, W, T, ED, C,
+    TGMS_LAUNCH(k_sample, dim3((unsigned)blocks), dim3(W64 * SW), 0, stream, B, seg_offsets, W, T, ED, C,
                        dt, yaw_mode, yaw_const, sample_offsets, out, pieces);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 }  // namespace tgms

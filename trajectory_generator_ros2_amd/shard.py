@@ -110,8 +110,9 @@ class ShardedBatch:
         me = dist.get_rank(group)
         cl = [torch.empty_like(Cp) for _ in range(self.world)] if me == dst else None
         sl = [torch.empty_like(Sp) for _ in range(self.world)] if me == dst else None
-        dist.gather(Cp, cl, dst=dst, group=group)
-        dist.gather(Sp, sl, dst=dst, group=group)
+        # `dst` is a rank of `group` (group_dst), compared with the group-local rank above
+        dist.gather(Cp, cl, group=group, group_dst=dst)
+        dist.gather(Sp, sl, group=group, group_dst=dst)
         if me != dst:
             return None
         Call = torch.cat([cl[r][: int(seg_per_rank[r])] for r in range(self.world)])
@@ -148,5 +149,5 @@ def pipelined_gather(solve_chunk: Callable, coeffs, chunks: int, dst: int = 0, o
             continue
         solve_chunk(lo, hi)
         gl = [out[r, lo:hi] for r in range(world)] if me == dst else None
-        works.append(dist.gather(coeffs[lo:hi], gl, dst=dst, group=group, async_op=True))
+        works.append(dist.gather(coeffs[lo:hi], gl, group=group, group_dst=dst, async_op=True))
     return works
