@@ -168,6 +168,43 @@ tgms_status tgms_sample_batch_device(tgms_handle* h, int32_t B, const int32_t* d
                                      const int64_t* d_sample_offsets, double* d_out,
                                      void* stream);
 
+/* ---- multi-GPU ----
+ * One process drives devices 0 .. device_count-1 through one handle that owns one RCCL
+ * communicator per device (ncclCommInitAll, rccl.h:236; RCCL is loaded here, not at
+ * library load).  The batch is split into contiguous shards of equal cost
+ * (tgms_plan_shards), every shard into pieces; device 0 scatters each piece's inputs
+ * to its device and gathers its coefficients / statuses back with grouped
+ * ncclSend / ncclRecv (rccl.h:700, :722; per-piece counts, so ragged batches need no
+ * padding) while the device solves the next piece.  Device 0 solves its own shard in
+ * place.  The caller sees one device-0 batch, exactly as tgms_solve_batch_device
+ * would produce it (identical coefficients: trajectories are independent).  The single-
+ * device entry points applied to a multi handle run on device 0 only; the multi entry
+ * points applied to a tgms_create handle run the single-device path.  Replaces nothing
+ * in the reference, whose caller (TrajectoryGenerator.hpp:83, src/TrajectoryGenerator.cpp:71)
+ * holds one Trajectory; this is the swarm / sampling planner's batch path (configs 4, 5). */
+tgms_status tgms_create_multi(tgms_handle** out, int device_count);
+int tgms_device_count(const tgms_handle* h); /* 1 for a tgms_create handle */
+/* Host-only shard planner: bounds [parts+1] of contiguous trajectory ranges with
+ * ~equal cost (reduced / band: 2 + M_b, dense KKT: (14 M_b + 2)^3 per trajectory). */
+tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t parts, int method,
+                             int32_t* bounds);
+/* Host pointers, blocking: upload to device 0, the multi-GPU solve, one download. */
+tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* seg_offsets,
+                                   const double* waypoints, const double* seg_times,
+                                   const double* end_derivs, double* coeffs, int32_t* status);
+/* Device-0 pointers, asynchronous on `stream` (a device-0 stream). */
+tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
+                                          const int32_t* d_seg_offsets, const double* d_waypoints,
+                                          const double* d_seg_times, const double* d_end_derivs,
+                                          double* d_coeffs, int32_t* d_status, void* stream);
+/* tgms_refine_loop_device over the devices (config 5): times (in place), costs,
+ * coefficients and statuses gathered back to device 0. */
+tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
+                                          const int32_t* d_seg_offsets, const double* d_waypoints,
+                                          double* d_seg_times, const double* d_end_derivs, double k_T,
+                                          double eta, int32_t iters, double* d_coeffs, double* d_cost,
+                                          int32_t* d_status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,108 @@
+"""The multi-GPU C ABI (tgms_create_multi & co., include/tgms.h) on one MI355X.
+
+With device_count = 1 device 0's shard is the whole batch, solved in place: the
+results must equal the single-device entry points bit for bit.  The RCCL pipeline
+(scatter of each piece's inputs, per-device solve, grouped send/recv gather) is then
+exercised on the one GPU with TGMS_MULTI_SELF_GATHER=1, which routes device 0's own
+shard through it (self send/recv on its communicator): again bit-equal, with end
+derivatives, a ragged batch, an invalid trajectory and the refinement loop.  N > 1
+runs only on an 8-GPU node (the driver's); DESIGN.md §6 records that it is unmeasured."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[False, True], ids=["in_place", "rccl_self_gather"])
+def multi(request):
+    from trajectory_generator_ros2_amd.solver import Solver
+    old = os.environ.pop("TGMS_MULTI_SELF_GATHER", None)
+    if request.param:
+        os.environ["TGMS_MULTI_SELF_GATHER"] = "1"  # read by tgms_create_multi
+    try:
+        s = Solver(device_count=1)
+    finally:
+        os.environ.pop("TGMS_MULTI_SELF_GATHER", None)
+        if old is not None:
+            os.environ["TGMS_MULTI_SELF_GATHER"] = old
+    assert s.device_count == 1
+    yield s
+    s.close()
+
+
+def _batch(kind):
+    from trajectory_generator_ros2_amd import synthetic as S
+    if kind == "uniform":
+        so, W, T = S.uniform_batch(5000, 10, seed=41)
+        return so, W.reshape(-1, 3), T.reshape(-1)
+    return S.ragged_batch(7001, 1, 16, seed=42)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "ragged"])
+def test_solve_multi_host_bit_equal(solver, multi, kind):
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG
+    so, W, T = _batch(kind)
+    T = T.copy()
+    T[int(so[123])] = -1.0  # trajectory 123 invalid
+    ED = np.random.default_rng(3).normal(size=(len(so) - 1, 18))
+    C1, st1, w1 = solver.solve(so, W, T, ED)
+    C2, st2, w2 = multi.solve_multi(so, W, T, ED)
+    assert w1 == w2 == ERR_INVALID_ARG and st2[123] == ERR_INVALID_ARG
+    np.testing.assert_array_equal(st1, st2)
+    np.testing.assert_array_equal(C1, C2)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "ragged"])
+def test_solve_multi_device_bit_equal(solver, multi, kind):
+    import torch
+    so, W, T = _batch(kind)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so.astype(np.int32)), d(W), d(T)
+    S = int(so[-1])
+    ref = torch.empty((S, 3, 8), dtype=torch.float64, device="cuda")
+    solver.solve_batch_device(so, dso, dW, dT, ref)
+    got = torch.full_like(ref, float("nan"))
+    st = torch.full((len(so) - 1,), -1, dtype=torch.int32, device="cuda")
+    multi.solve_batch_multi_device(so, dso, dW, dT, got, st)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert int(st.abs().sum()) == 0
+
+
+def test_refine_loop_multi_device_bit_equal(solver, multi):
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(3001, 2, 16, seed=43)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    B, Sg = len(so) - 1, int(so[-1])
+    outs = []
+    for s, fn in ((solver, solver.refine_loop_device), (multi, multi.refine_loop_multi_device)):
+        dso, dW, dT = d(so.astype(np.int32)), d(W), d(T.copy())
+        dC = torch.full((Sg, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+        dcost = torch.full((B,), float("nan"), dtype=torch.float64, device="cuda")
+        dst = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+        fn(so, dso, dW, dT, 1.0, 0.1, 10, dC, dcost, dst)
+        torch.cuda.synchronize()
+        outs.append((dT.cpu().numpy(), dC.cpu().numpy(), dcost.cpu().numpy(), dst.cpu().numpy()))
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    assert not np.array_equal(outs[0][0], T)
+
+
+def test_multi_handle_single_device_calls_and_errors(multi):
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_UNSUPPORTED, METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(64, 4, seed=5)
+    C, st, w = multi.solve(so, W.reshape(-1, 3), T.reshape(-1))  # single-device call on device 0
+    assert w == 0
+    C2, st2, w2 = multi.solve_multi(so, W.reshape(-1, 3), T.reshape(-1))
+    np.testing.assert_array_equal(C, C2)
+    assert multi.solve_multi(np.array([0, 0], np.int32), np.zeros((1, 3)), np.zeros(0))[2] == ERR_INVALID_ARG
+    so11, W11, T11 = S.uniform_batch(4, 11, seed=1)
+    multi.set_method(METHOD_DENSE_KKT)
+    try:
+        assert multi.solve_multi(so11, W11.reshape(-1, 3), T11.reshape(-1))[2] == ERR_UNSUPPORTED
+    finally:
+        multi.set_method(METHOD_REDUCED)

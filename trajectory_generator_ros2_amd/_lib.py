@@ -25,6 +25,8 @@ EXPORTS = [
     "tgms_set_method", "tgms_solve_batch", "tgms_solve_uniform_device", "tgms_solve_batch_device",
     "tgms_sample_count", "tgms_sample_offsets", "tgms_sample_batch", "tgms_sample_batch_device",
     "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_loop_device", "tgms_refine_batch",
+    "tgms_create_multi", "tgms_device_count", "tgms_plan_shards", "tgms_solve_batch_multi",
+    "tgms_solve_batch_multi_device", "tgms_refine_loop_multi_device",
 ]
 
 _lib = None
@@ -87,6 +89,18 @@ def load(path: str = ""):
     L.tgms_refine_loop_device.restype = ctypes.c_int
     L.tgms_refine_batch.argtypes = [vp, i32, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp]
     L.tgms_refine_batch.restype = ctypes.c_int
+    L.tgms_create_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.tgms_create_multi.restype = ctypes.c_int
+    L.tgms_device_count.argtypes = [vp]
+    L.tgms_device_count.restype = ctypes.c_int
+    L.tgms_plan_shards.argtypes = [i32, vp, i32, ctypes.c_int, vp]
+    L.tgms_plan_shards.restype = ctypes.c_int
+    L.tgms_solve_batch_multi.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+    L.tgms_solve_batch_multi.restype = ctypes.c_int
+    L.tgms_solve_batch_multi_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.tgms_solve_batch_multi_device.restype = ctypes.c_int
+    L.tgms_refine_loop_multi_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp, vp]
+    L.tgms_refine_loop_multi_device.restype = ctypes.c_int
     if L.tgms_abi_version() != ABI_VERSION:
         raise ImportError(f"libtgms ABI {L.tgms_abi_version()} != {ABI_VERSION}")
     _lib = L

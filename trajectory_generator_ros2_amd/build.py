@@ -60,7 +60,7 @@ def build_tgms(force: bool = False) -> str:
     with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
         list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))
     if force or todo or _newer(LIB_TGMS, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TGMS] + objs)
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TGMS] + objs + ["-ldl"])
     return LIB_TGMS
 
 

@@ -10,7 +10,9 @@
 #include "tgms.h"
 #include "tgms_internal.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -25,8 +27,11 @@
 #define TGMS_AUX_STREAMS 4
 #endif
 
+struct tgms_multi_ctx;  // multi-GPU state of a tgms_create_multi handle (below)
+
 struct tgms_handle {
     int device = 0;
+    tgms_multi_ctx* multi = nullptr;  // non-null: handle over devices 0..n-1 (tgms_create_multi)
     int method = TGMS_METHOD_REDUCED;
     hipStream_t stream = nullptr;  // stream of the blocking (host-pointer) API
     std::string last_error;
@@ -200,13 +205,16 @@ tgms_status upload_plan(tgms_handle* h, int32_t B, const int32_t* so,
 struct Plan {
     int uniform_m = 0;
     std::vector<int32_t> counts, starts;
+    const int32_t* d_perm = nullptr;  // ragged: trajectory ids grouped by M (device)
 };
 
 tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m, Plan* p, hipStream_t stream) {
     tgms_status s = check_offsets(h, B, h_so, max_m, &p->counts, &p->uniform_m);
     if (s != TGMS_OK || B == 0) return s;
-    if (p->uniform_m <= 0) return upload_plan(h, B, h_so, p->counts, &p->starts, stream);
-    return TGMS_OK;
+    if (p->uniform_m > 0) return TGMS_OK;
+    s = upload_plan(h, B, h_so, p->counts, &p->starts, stream);
+    p->d_perm = h->d_perm;
+    return s;
 }
 
 tgms_status ensure_aux(tgms_handle* h) {
@@ -271,7 +279,7 @@ tgms_status run_chains(tgms_handle* h, hipStream_t stream,
 
 // Reduced method, ragged plan: every M group in one launch per occupancy class
 // (M <= 11 / M >= 12), the longest groups' wavefronts first.
-void class_tables(const tgms_handle* h, const Plan& p, tgms::GroupTable (&tab)[2]) {
+void class_tables(const Plan& p, tgms::GroupTable (&tab)[2]) {
     tab[0] = tgms::GroupTable{};
     tab[1] = tgms::GroupTable{};
     for (size_t m = p.counts.size(); m-- > 1;) {
@@ -280,7 +288,7 @@ void class_tables(const tgms_handle* h, const Plan& p, tgms::GroupTable (&tab)[2
         const int g = t.ngroups++;
         t.m[g] = (int32_t)m;
         t.n[g] = p.counts[m];
-        t.perm[g] = h->d_perm + p.starts[m];
+        t.perm[g] = p.d_perm + p.starts[m];
         t.blk_end[g] = (g ? t.blk_end[g - 1] : 0) + (p.counts[m] + tgms::RAGGED_TPW - 1) / tgms::RAGGED_TPW;
     }
 }
@@ -289,7 +297,7 @@ tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, 
                              const double* W, const double* T, const double* ED, double kT, double eta,
                              double* Tout, double* cost, double* C, int32_t* st) {
     tgms::GroupTable tab[2];
-    class_tables(h, p, tab);
+    class_tables(p, tab);
     std::vector<std::function<hipError_t(hipStream_t)>> jobs;
     for (int c = 1; c >= 0; --c)
         if (tab[c].ngroups)
@@ -337,7 +345,7 @@ tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_
         }
         for (size_t m = p.counts.size(); m-- > 1;)
             if (p.counts[m])
-                TGMS_HIP(h, tgms::launch_band_kkt((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED, C,
+                TGMS_HIP(h, tgms::launch_band_kkt((int)m, p.counts[m], p.d_perm + p.starts[m], d_so, W, T, ED, C,
                                                   st, h->d_band, h->band_grid, stream));
         return TGMS_OK;
     }
@@ -354,7 +362,7 @@ tgms_status dispatch(tgms_handle* h, const Plan& p, int32_t B, const int32_t* d_
     for (size_t m = p.counts.size(); m-- > 1;)
         if (p.counts[m])
             jobs.push_back([&, m](hipStream_t q) {
-                return tgms::launch_dense_kkt((int)m, p.counts[m], h->d_perm + p.starts[m], d_so, W, T, ED, C, st, q);
+                return tgms::launch_dense_kkt((int)m, p.counts[m], p.d_perm + p.starts[m], d_so, W, T, ED, C, st, q);
             });
     return run_parallel(h, stream, jobs);
 }
@@ -384,7 +392,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         // times kept in LDS between steps and updated in place in T[0]; the two classes'
         // launches run side by side.
         tgms::GroupTable tab[2];
-        class_tables(h, p, tab);
+        class_tables(p, tab);
         std::vector<std::function<hipError_t(hipStream_t)>> jobs;
         for (int k = 1; k >= 0; --k)
             if (tab[k].ngroups)
@@ -403,7 +411,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         // the end; neither waits for the other's step (each class alone fills ~2/3 of
         // the GPU).
         tgms::GroupTable tab[2];
-        class_tables(h, p, tab);
+        class_tables(p, tab);
         // one op list per class; ops are issued round-robin across the classes so a
         // captured graph holds them interleaved and launches both chains side by side
         // (capturing one whole chain first held the other back by its ~80 us of
@@ -464,6 +472,435 @@ int max_m_for(const tgms_handle* h) {
     return h->method == TGMS_METHOD_DENSE_KKT ? TGMS_DENSE_MAX_SEGMENTS : TGMS_MAX_SEGMENTS;
 }
 
+// ---------------------------------------------------------------------------
+// Multi-GPU handle: one process drives devices 0..n-1 through
+// one communicator per device (ncclCommInitAll, rccl.h:236).  A batch is split into
+// contiguous cost-balanced shards (plan_shards: the same rule as shard.ragged_bounds);
+// every shard is cut into pieces; device 0 scatters each piece's inputs to its device
+// over RCCL (grouped ncclSend/ncclRecv, rccl.h:700/722: per-piece byte counts, so
+// ragged batches need no padding), the device solves the piece on its compute stream,
+// and the piece's coefficients (+ statuses, and for the refinement loop its times and
+// costs) go back to device 0 on the device's communication stream while the next
+// piece is being solved.  Device 0's own shard is solved in place on the caller's
+// stream, beside the gathers.  RCCL is loaded at tgms_create_multi (dlopen), so
+// single-device users never load it.
+
+struct RcclApi {
+    void* lib = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+
+    bool load(std::string* err) {
+        // librccl.so.1 is torch's bundled copy when torch is loaded (same soname), else ROCm's
+        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+            lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (lib) break;
+        }
+        if (!lib) {
+            *err = std::string("cannot load RCCL (librccl.so.1): ") + dlerror();
+            return false;
+        }
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+            return fn != nullptr;
+        };
+        if (sym(comm_init_all, "ncclCommInitAll") && sym(comm_destroy, "ncclCommDestroy") && sym(send, "ncclSend") &&
+            sym(recv, "ncclRecv") && sym(group_start, "ncclGroupStart") && sym(group_end, "ncclGroupEnd") &&
+            sym(error_string, "ncclGetErrorString"))
+            return true;
+        *err = "RCCL library lacks a needed entry point";
+        return false;
+    }
+};
+
+// Contiguous cost-balanced shards of a CSR batch: the rule of shard.ragged_bounds
+// (trajectory_generator_ros2_amd/shard.py), step for step in the same fp64 arithmetic,
+// so the C++ and Python planners give identical bounds (tests/test_multi_host.py).
+void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* bounds) {
+    bounds[0] = 0;
+    if (B == 0) {
+        for (int k = 1; k <= parts; ++k) bounds[k] = 0;
+        return;
+    }
+    std::vector<double> c(B);
+    double acc = 0.0;
+    for (int32_t b = 0; b < B; ++b) {
+        const double m = (double)(so[b + 1] - so[b]);
+        const double cost = method == TGMS_METHOD_DENSE_KKT ? (14.0 * m + 2.0) * (14.0 * m + 2.0) * (14.0 * m + 2.0)
+                                                            : 2.0 + m;
+        acc += cost;
+        c[b] = acc;
+    }
+    int64_t prev = 0;
+    for (int k = 1; k < parts; ++k) {
+        const double target = (c[B - 1] * (double)k) / (double)parts;
+        int64_t cut = (int64_t)(std::lower_bound(c.begin(), c.end(), target) - c.begin()) + 1;
+        cut = std::max(cut, prev);  // running maximum, then capped at B
+        prev = cut;
+        bounds[k] = (int32_t)std::min<int64_t>(cut, B);
+    }
+    bounds[parts] = B;
+}
+
+constexpr int MULTI_PIECES = 4;  // pieces per shard: the gather of piece p overlaps the solve of p + 1
+
+enum class MultiJob { Solve, Refine };
+
+struct MultiArgs {
+    MultiJob job = MultiJob::Solve;
+    int32_t B = 0;
+    const int32_t* h_so = nullptr;
+    const int32_t* d_so = nullptr;  // device 0
+    const double *dW = nullptr, *dED = nullptr;
+    double* dT = nullptr;  // refine: updated in place
+    double *dC = nullptr, *d_cost = nullptr;
+    int32_t* dSt = nullptr;
+    double k_T = 0.0, eta = 0.0;
+    int32_t iters = 0;
+};
+
+// One piece of one device's shard: trajectories [lo, hi) of the batch, and the byte
+// offsets of its arrays inside the device's piece workspace.
+struct Piece {
+    int32_t lo = 0, hi = 0;
+    int64_t s0 = 0, s1 = 0;  // segment range
+    size_t oW = 0, oT = 0, oT2 = 0, oED = 0, oC = 0, oSt = 0, oCost = 0, oSo = 0, oPerm = 0;
+    Plan plan;
+    int32_t n() const { return hi - lo; }
+    int64_t S() const { return s1 - s0; }
+};
+
+}  // namespace
+
+struct tgms_multi_ctx {
+    int n = 0;
+    RcclApi r;
+    std::vector<ncclComm_t> comm;
+    std::vector<tgms_handle*> sub;    // sub[0] is the root handle itself
+    std::vector<hipStream_t> sm;      // per device: RCCL stream (sm[0]: device 0's scatter/gather stream)
+    std::vector<hipStream_t> sc;      // per device: compute stream of its pieces
+    std::vector<char*> dws;           // per device: piece workspace (device)
+    std::vector<size_t> dws_cap;
+    std::vector<char*> pin;           // per device: pinned staging of the pieces' plans
+    std::vector<size_t> pin_cap;
+    std::vector<hipEvent_t> ev_up, ev_in;
+    std::vector<bool> up_pending;
+    std::vector<std::vector<hipEvent_t>> ev_piece;
+    hipEvent_t ev_start = nullptr, ev_end = nullptr;
+    bool self_gather = false;  // device 0's shard through the RCCL pipeline too (tests on one GPU)
+};
+
+namespace {
+
+tgms_status nccl_err(tgms_handle* h, ncclResult_t e, const char* where) {
+    if (e == ncclSuccess) return TGMS_OK;
+    const char* msg = h->multi && h->multi->r.error_string ? h->multi->r.error_string(e) : "RCCL error";
+    return set_err(h, TGMS_ERR_DEVICE, std::string(where) + ": " + msg);
+}
+#define TGMS_NCCL(h, call)                                    \
+    do {                                                      \
+        ncclResult_t n_ = (call);                             \
+        if (n_ != ncclSuccess) return nccl_err(h, n_, #call); \
+    } while (0)
+
+void destroy_multi(tgms_multi_ctx* m) {
+    if (!m) return;
+    for (int d = 0; d < m->n; ++d) {
+        (void)hipSetDevice(d);
+        (void)hipDeviceSynchronize();
+    }
+    for (int d = 0; d < m->n; ++d) {
+        if (d < (int)m->comm.size() && m->comm[d] && m->r.comm_destroy) (void)m->r.comm_destroy(m->comm[d]);
+        (void)hipSetDevice(d);
+        if (d < (int)m->sm.size() && m->sm[d]) (void)hipStreamDestroy(m->sm[d]);
+        if (d == 0 && d < (int)m->sc.size() && m->sc[d]) (void)hipStreamDestroy(m->sc[d]);
+        if (d < (int)m->dws.size() && m->dws[d]) (void)hipFree(m->dws[d]);
+        if (d < (int)m->pin.size() && m->pin[d]) (void)hipHostFree(m->pin[d]);
+        if (d < (int)m->ev_up.size() && m->ev_up[d]) (void)hipEventDestroy(m->ev_up[d]);
+        if (d < (int)m->ev_in.size() && m->ev_in[d]) (void)hipEventDestroy(m->ev_in[d]);
+        if (d < (int)m->ev_piece.size())
+            for (hipEvent_t e : m->ev_piece[d])
+                if (e) (void)hipEventDestroy(e);
+        if (d >= 1 && d < (int)m->sub.size() && m->sub[d]) tgms_destroy(m->sub[d]);
+    }
+    (void)hipSetDevice(0);
+    if (m->ev_start) (void)hipEventDestroy(m->ev_start);
+    if (m->ev_end) (void)hipEventDestroy(m->ev_end);
+    delete m;
+}
+
+// Counting sort of one piece's trajectories by M into `perm` (host); fills the plan's
+// counts / starts / uniform_m (as check_offsets + upload_plan do for a whole batch).
+void piece_plan(const int32_t* so_rebased, int32_t n, int max_m, Plan* p, int32_t* perm) {
+    p->counts.assign(max_m + 1, 0);
+    int um = -1;
+    for (int32_t b = 0; b < n; ++b) {
+        const int32_t M = so_rebased[b + 1] - so_rebased[b];
+        p->counts[M]++;
+        um = (b == 0) ? M : (um == M ? M : 0);
+    }
+    p->uniform_m = n > 0 ? um : 0;
+    p->starts.assign(p->counts.size() + 1, 0);
+    for (size_t m = 1; m < p->counts.size(); ++m) p->starts[m + 1] = p->starts[m] + p->counts[m];
+    if (p->uniform_m > 0) return;
+    std::vector<int32_t> fill(p->starts.begin(), p->starts.end());
+    for (int32_t b = 0; b < n; ++b) perm[fill[so_rebased[b + 1] - so_rebased[b]]++] = b;
+}
+
+// The multi-GPU pipeline (see the section comment).  Arrays in `a` live on device 0
+// and are ordered on `ustream` (a device-0 stream).
+tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
+    tgms_multi_ctx* m = h->multi;
+    const int n = m->n;
+    const bool refine = a.job == MultiJob::Refine;
+    const int max_m = refine ? TGMS_MAX_SEGMENTS : max_m_for(h);
+    std::vector<int32_t> bounds(n + 1);
+    plan_shards(a.B, a.h_so, n, h->method, bounds.data());
+    // pieces of every device that goes through the RCCL pipeline
+    std::vector<std::vector<Piece>> pieces(n);
+    for (int d = 0; d < n; ++d) {
+        if (d == 0 && !m->self_gather) continue;
+        const int32_t lo = bounds[d], hi = bounds[d + 1];
+        if (hi <= lo) continue;
+        std::vector<int32_t> so_l(hi - lo + 1);
+        for (int32_t b = lo; b <= hi; ++b) so_l[b - lo] = a.h_so[b] - a.h_so[lo];
+        int32_t pb[MULTI_PIECES + 1];
+        plan_shards(hi - lo, so_l.data(), MULTI_PIECES, h->method, pb);
+        size_t plan_bytes = 0, off = 0;
+        for (int k = 0; k < MULTI_PIECES; ++k) {
+            if (pb[k + 1] <= pb[k]) continue;
+            Piece p;
+            p.lo = lo + pb[k];
+            p.hi = lo + pb[k + 1];
+            p.s0 = a.h_so[p.lo];
+            p.s1 = a.h_so[p.hi];
+            p.oSo = plan_bytes;
+            plan_bytes = align256(plan_bytes + sizeof(int32_t) * (p.n() + 1));
+            p.oPerm = plan_bytes;
+            plan_bytes = align256(plan_bytes + sizeof(int32_t) * p.n());
+            pieces[d].push_back(p);
+        }
+        off = plan_bytes;  // the plan block (mirrored in the pinned staging) comes first
+        for (Piece& p : pieces[d]) {
+            p.oW = off; off = align256(off + 8 * (size_t)(p.S() + p.n()) * 3);
+            p.oT = off; off = align256(off + 8 * (size_t)p.S());
+            p.oT2 = off; off = align256(off + (refine ? 8 * (size_t)p.S() : 0));
+            p.oED = off; off = align256(off + (a.dED ? 8 * (size_t)p.n() * 18 : 0));
+            p.oC = off; off = align256(off + (a.dC ? 8 * (size_t)p.S() * 24 : 0));
+            p.oSt = off; off = align256(off + 4 * (size_t)p.n());
+            p.oCost = off; off = align256(off + (refine ? 8 * (size_t)p.n() : 0));
+        }
+        // workspaces (grow-only; a regrow waits for the device's previous work)
+        TGMS_HIP(h, hipSetDevice(d));
+        if (off > m->dws_cap[d]) {
+            TGMS_HIP(h, hipDeviceSynchronize());
+            if (m->dws[d]) TGMS_HIP(h, hipFree(m->dws[d]));
+            m->dws[d] = nullptr;
+            m->dws_cap[d] = 0;
+            TGMS_HIP(h, hipMalloc(reinterpret_cast<void**>(&m->dws[d]), off));
+            m->dws_cap[d] = off;
+        }
+        if (m->up_pending[d]) TGMS_HIP(h, hipEventSynchronize(m->ev_up[d]));  // staging free again
+        m->up_pending[d] = false;
+        if (plan_bytes > m->pin_cap[d]) {
+            if (m->pin[d]) TGMS_HIP(h, hipHostFree(m->pin[d]));
+            m->pin[d] = nullptr;
+            m->pin_cap[d] = 0;
+            TGMS_HIP(h, hipHostMalloc(reinterpret_cast<void**>(&m->pin[d]), plan_bytes));
+            m->pin_cap[d] = plan_bytes;
+        }
+        for (Piece& p : pieces[d]) {
+            int32_t* so_p = reinterpret_cast<int32_t*>(m->pin[d] + p.oSo);
+            for (int32_t b = p.lo; b <= p.hi; ++b) so_p[b - p.lo] = a.h_so[b] - a.h_so[p.lo];
+            piece_plan(so_p, p.n(), max_m, &p.plan, reinterpret_cast<int32_t*>(m->pin[d] + p.oPerm));
+            p.plan.d_perm = reinterpret_cast<const int32_t*>(m->dws[d] + p.oPerm);
+        }
+        if (plan_bytes) {
+            TGMS_HIP(h, hipMemcpyAsync(m->dws[d], m->pin[d], plan_bytes, hipMemcpyHostToDevice, m->sc[d]));
+            TGMS_HIP(h, hipEventRecord(m->ev_up[d], m->sc[d]));
+            m->up_pending[d] = true;
+        }
+    }
+    // device 0: the caller's inputs are ready on ustream
+    TGMS_HIP(h, hipSetDevice(0));
+    TGMS_HIP(h, hipEventRecord(m->ev_start, ustream));
+    TGMS_HIP(h, hipStreamWaitEvent(m->sm[0], m->ev_start, 0));
+    // scatter: every piece's inputs from device 0 into its device's workspace
+    TGMS_NCCL(h, m->r.group_start());
+    for (int d = 0; d < n; ++d)
+        for (const Piece& p : pieces[d]) {
+            char* w = m->dws[d];
+            const size_t nw = (size_t)(p.S() + p.n()) * 3, nt = (size_t)p.S(), ne = (size_t)p.n() * 18;
+            TGMS_NCCL(h, m->r.send(a.dW + (p.s0 + p.lo) * 3, nw, ncclFloat64, d, m->comm[0], m->sm[0]));
+            TGMS_NCCL(h, m->r.recv(w + p.oW, nw, ncclFloat64, 0, m->comm[d], m->sm[d]));
+            TGMS_NCCL(h, m->r.send(a.dT + p.s0, nt, ncclFloat64, d, m->comm[0], m->sm[0]));
+            TGMS_NCCL(h, m->r.recv(w + p.oT, nt, ncclFloat64, 0, m->comm[d], m->sm[d]));
+            if (a.dED) {
+                TGMS_NCCL(h, m->r.send(a.dED + (size_t)p.lo * 18, ne, ncclFloat64, d, m->comm[0], m->sm[0]));
+                TGMS_NCCL(h, m->r.recv(w + p.oED, ne, ncclFloat64, 0, m->comm[d], m->sm[d]));
+            }
+        }
+    TGMS_NCCL(h, m->r.group_end());
+    for (int d = 0; d < n; ++d) {
+        if (pieces[d].empty()) continue;
+        TGMS_HIP(h, hipSetDevice(d));
+        TGMS_HIP(h, hipEventRecord(m->ev_in[d], m->sm[d]));
+        TGMS_HIP(h, hipStreamWaitEvent(m->sc[d], m->ev_in[d], 0));
+    }
+    // device 0's own shard, in place on the caller's stream (beside the gathers)
+    TGMS_HIP(h, hipSetDevice(0));
+    if (!m->self_gather && bounds[1] > 0) {
+        const int32_t b1 = bounds[1];
+        tgms_status s = scratch_acquire(h, ustream);
+        if (s != TGMS_OK) return s;
+        Plan p0;
+        s = make_plan(h, b1, a.h_so, max_m, &p0, ustream);
+        if (s != TGMS_OK) return s;
+        if (refine) {
+            const size_t S0 = (size_t)a.h_so[b1];
+            s = ensure_loop_ws(h, align256(S0 * 8));
+            if (s != TGMS_OK) return s;
+            double* T[2] = {a.dT, h->d_loop_ws};
+            int cur = 0;
+            s = refine_loop(h, p0, b1, a.d_so, a.dW, T, a.dED, a.k_T, a.eta, a.iters, a.dC, a.d_cost, a.dSt, ustream,
+                            &cur);
+            if (s == TGMS_OK && cur == 1)
+                TGMS_HIP(h, hipMemcpyAsync(a.dT, T[1], S0 * 8, hipMemcpyDeviceToDevice, ustream));
+        } else {
+            s = dispatch(h, p0, b1, a.d_so, a.dW, a.dT, a.dED, a.dC, a.dSt, ustream);
+        }
+        if (s == TGMS_OK) s = scratch_release(h, ustream);
+        if (s != TGMS_OK) return s;
+    }
+    // pieces: solve on the device, then gather to device 0 beside the next piece's solve
+    for (int k = 0; k < MULTI_PIECES; ++k) {
+        bool any = false;
+        for (int d = 0; d < n; ++d) {
+            if (k >= (int)pieces[d].size()) continue;
+            any = true;
+            const Piece& p = pieces[d][k];
+            char* w = m->dws[d];
+            tgms_handle* hd = m->sub[d];
+            TGMS_HIP(h, hipSetDevice(d));
+            const int32_t* so_p = reinterpret_cast<const int32_t*>(w + p.oSo);
+            double* Wp = reinterpret_cast<double*>(w + p.oW);
+            double* Tp = reinterpret_cast<double*>(w + p.oT);
+            const double* EDp = a.dED ? reinterpret_cast<const double*>(w + p.oED) : nullptr;
+            double* Cp = a.dC ? reinterpret_cast<double*>(w + p.oC) : nullptr;
+            int32_t* Stp = reinterpret_cast<int32_t*>(w + p.oSt);
+            tgms_status s;
+            if (refine) {
+                double* T[2] = {Tp, reinterpret_cast<double*>(w + p.oT2)};
+                int cur = 0;
+                s = refine_loop(hd, p.plan, p.n(), so_p, Wp, T, EDp, a.k_T, a.eta, a.iters, Cp,
+                                reinterpret_cast<double*>(w + p.oCost), Stp, m->sc[d], &cur);
+                if (s == TGMS_OK && cur == 1)
+                    TGMS_HIP(h, hipMemcpyAsync(Tp, T[1], (size_t)p.S() * 8, hipMemcpyDeviceToDevice, m->sc[d]));
+            } else {
+                s = dispatch(hd, p.plan, p.n(), so_p, Wp, Tp, EDp, Cp, Stp, m->sc[d]);
+            }
+            if (s != TGMS_OK) return hd == h ? s : set_err(h, s, std::string("device ") + std::to_string(d) + ": " +
+                                                                 tgms_last_error(hd));
+            TGMS_HIP(h, hipEventRecord(m->ev_piece[d][k], m->sc[d]));
+            TGMS_HIP(h, hipStreamWaitEvent(m->sm[d], m->ev_piece[d][k], 0));
+        }
+        if (!any) break;
+        TGMS_NCCL(h, m->r.group_start());
+        for (int d = 0; d < n; ++d) {
+            if (k >= (int)pieces[d].size()) continue;
+            const Piece& p = pieces[d][k];
+            char* w = m->dws[d];
+            if (a.dC) {
+                TGMS_NCCL(h, m->r.send(w + p.oC, (size_t)p.S() * 24, ncclFloat64, 0, m->comm[d], m->sm[d]));
+                TGMS_NCCL(h, m->r.recv(a.dC + p.s0 * 24, (size_t)p.S() * 24, ncclFloat64, d, m->comm[0], m->sm[0]));
+            }
+            if (a.dSt) {
+                TGMS_NCCL(h, m->r.send(w + p.oSt, (size_t)p.n(), ncclInt32, 0, m->comm[d], m->sm[d]));
+                TGMS_NCCL(h, m->r.recv(a.dSt + p.lo, (size_t)p.n(), ncclInt32, d, m->comm[0], m->sm[0]));
+            }
+            if (refine) {
+                TGMS_NCCL(h, m->r.send(w + p.oT, (size_t)p.S(), ncclFloat64, 0, m->comm[d], m->sm[d]));
+                TGMS_NCCL(h, m->r.recv(a.dT + p.s0, (size_t)p.S(), ncclFloat64, d, m->comm[0], m->sm[0]));
+                if (a.d_cost) {
+                    TGMS_NCCL(h, m->r.send(w + p.oCost, (size_t)p.n(), ncclFloat64, 0, m->comm[d], m->sm[d]));
+                    TGMS_NCCL(h, m->r.recv(a.d_cost + p.lo, (size_t)p.n(), ncclFloat64, d, m->comm[0], m->sm[0]));
+                }
+            }
+        }
+        TGMS_NCCL(h, m->r.group_end());
+    }
+    TGMS_HIP(h, hipSetDevice(0));
+    TGMS_HIP(h, hipEventRecord(m->ev_end, m->sm[0]));
+    TGMS_HIP(h, hipStreamWaitEvent(ustream, m->ev_end, 0));
+    return TGMS_OK;
+}
+
+tgms_status create_multi_ctx(tgms_handle* h, int n) {
+    tgms_multi_ctx* m = new tgms_multi_ctx();
+    h->multi = m;
+    m->n = n;
+    const char* sg = std::getenv("TGMS_MULTI_SELF_GATHER");
+    m->self_gather = sg && sg[0] == '1';
+    std::string err;
+    if (!m->r.load(&err)) return set_err(h, TGMS_ERR_DEVICE, err);
+    m->comm.assign(n, nullptr);
+    m->sub.assign(n, nullptr);
+    m->sm.assign(n, nullptr);
+    m->sc.assign(n, nullptr);
+    m->dws.assign(n, nullptr);
+    m->dws_cap.assign(n, 0);
+    m->pin.assign(n, nullptr);
+    m->pin_cap.assign(n, 0);
+    m->ev_up.assign(n, nullptr);
+    m->ev_in.assign(n, nullptr);
+    m->up_pending.assign(n, false);
+    m->ev_piece.assign(n, std::vector<hipEvent_t>(MULTI_PIECES, nullptr));
+    std::vector<int> devs(n);
+    for (int d = 0; d < n; ++d) devs[d] = d;
+    TGMS_NCCL(h, m->r.comm_init_all(m->comm.data(), n, devs.data()));
+    m->sub[0] = h;
+    for (int d = 0; d < n; ++d) {
+        if (d >= 1) {
+            const tgms_status s = tgms_create(&m->sub[d], d);
+            if (s != TGMS_OK) return set_err(h, s, "tgms_create on device " + std::to_string(d));
+            m->sub[d]->method = h->method;
+        }
+        TGMS_HIP(h, hipSetDevice(d));
+        TGMS_HIP(h, hipStreamCreateWithFlags(&m->sm[d], hipStreamNonBlocking));
+        if (d == 0)
+            TGMS_HIP(h, hipStreamCreateWithFlags(&m->sc[0], hipStreamNonBlocking));
+        else
+            m->sc[d] = m->sub[d]->stream;
+        TGMS_HIP(h, hipEventCreateWithFlags(&m->ev_up[d], hipEventDisableTiming));
+        TGMS_HIP(h, hipEventCreateWithFlags(&m->ev_in[d], hipEventDisableTiming));
+        for (auto& e : m->ev_piece[d]) TGMS_HIP(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    TGMS_HIP(h, hipSetDevice(0));
+    TGMS_HIP(h, hipEventCreateWithFlags(&m->ev_start, hipEventDisableTiming));
+    TGMS_HIP(h, hipEventCreateWithFlags(&m->ev_end, hipEventDisableTiming));
+    return TGMS_OK;
+}
+
+tgms_status worst_status(tgms_handle* h, const int32_t* st, int32_t B) {
+    int worst = TGMS_OK;
+    for (int32_t b = 0; b < B; ++b) worst = std::max(worst, (int)st[b]);
+    if (worst != TGMS_OK) {
+        for (int32_t b = 0; b < B; ++b)
+            if (st[b] == worst) {
+                char buf[160];
+                snprintf(buf, sizeof buf, "trajectory %d: %s", b, tgms_status_string(worst));
+                h->last_error = buf;
+                break;
+            }
+    }
+    return (tgms_status)worst;
+}
+
 }  // namespace
 
 extern "C" {
@@ -504,6 +941,10 @@ tgms_status tgms_create(tgms_handle** out, int device) {
 
 void tgms_destroy(tgms_handle* h) {
     if (!h) return;
+    if (h->multi) {
+        destroy_multi(h->multi);
+        h->multi = nullptr;
+    }
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     (void)hipDeviceSynchronize();
@@ -532,6 +973,9 @@ tgms_status tgms_set_method(tgms_handle* h, int method) {
     if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT && method != TGMS_METHOD_BAND_KKT)
         return set_err(h, TGMS_ERR_INVALID_ARG, "unknown method");
     h->method = method;
+    if (h->multi)
+        for (tgms_handle* sub : h->multi->sub)
+            if (sub) sub->method = method;
     return TGMS_OK;
 }
 
@@ -914,6 +1358,155 @@ tgms_status tgms_sample_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     TGMS_HIP(h, hipMemcpyAsync(out, dOut, nS * TGMS_GOAL_STRIDE * 8, hipMemcpyDeviceToHost, st));
     TGMS_HIP(h, hipStreamSynchronize(st));
     return TGMS_OK;
+}
+
+// ---- multi-GPU ----
+
+tgms_status tgms_create_multi(tgms_handle** out, int device_count) {
+    if (!out) return TGMS_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return TGMS_ERR_NO_DEVICE;
+    if (device_count < 1 || device_count > n) return TGMS_ERR_INVALID_ARG;
+    tgms_handle* h = nullptr;
+    tgms_status s = tgms_create(&h, 0);
+    if (s != TGMS_OK) return s;
+    s = create_multi_ctx(h, device_count);
+    if (s != TGMS_OK) {
+        fprintf(stderr, "tgms_create_multi: %s\n", h->last_error.c_str());
+        tgms_destroy(h);
+        return s;
+    }
+    *out = h;
+    return TGMS_OK;
+}
+
+int tgms_device_count(const tgms_handle* h) { return !h ? 0 : (h->multi ? h->multi->n : 1); }
+
+tgms_status tgms_plan_shards(int32_t B, const int32_t* so, int32_t parts, int method, int32_t* bounds) {
+    if (parts < 1 || !bounds || B < 0 || !so || so[0] != 0) return TGMS_ERR_INVALID_ARG;
+    if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT && method != TGMS_METHOD_BAND_KKT)
+        return TGMS_ERR_INVALID_ARG;
+    for (int32_t b = 0; b < B; ++b)
+        if (so[b + 1] - so[b] < 1) return TGMS_ERR_INVALID_ARG;
+    plan_shards(B, so, parts, method, bounds);
+    return TGMS_OK;
+}
+
+tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32_t* h_so, const int32_t* d_so,
+                                          const double* dW, const double* dT, const double* dED, double* dC,
+                                          int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    if (!h->multi) return tgms_solve_batch_device(h, B, h_so, d_so, dW, dT, dED, dC, dSt, stream);
+    h->last_error.clear();
+    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), nullptr, nullptr);
+    if (s != TGMS_OK || B == 0) return s;
+    if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
+    MultiArgs a;
+    a.job = MultiJob::Solve;
+    a.B = B;
+    a.h_so = h_so;
+    a.d_so = d_so;
+    a.dW = dW;
+    a.dT = const_cast<double*>(dT);  // read only for a solve
+    a.dED = dED;
+    a.dC = dC;
+    a.dSt = dSt;
+    s = multi_run(h, a, static_cast<hipStream_t>(stream));
+    (void)hipSetDevice(h->device);
+    return s;
+}
+
+tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32_t* h_so, const int32_t* d_so,
+                                          const double* dW, double* dT, const double* dED, double k_T, double eta,
+                                          int32_t iters, double* dC, double* d_cost, int32_t* dSt, void* stream) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    if (!h->multi)
+        return tgms_refine_loop_device(h, B, h_so, d_so, dW, dT, dED, k_T, eta, iters, dC, d_cost, dSt, stream);
+    h->last_error.clear();
+    tgms_status s = check_refine_args(h, k_T, eta);
+    if (s != TGMS_OK) return s;
+    if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    if (s != TGMS_OK || B == 0) return s;
+    if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
+    TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
+    MultiArgs a;
+    a.job = MultiJob::Refine;
+    a.B = B;
+    a.h_so = h_so;
+    a.d_so = d_so;
+    a.dW = dW;
+    a.dT = dT;
+    a.dED = dED;
+    a.dC = dC;
+    a.d_cost = d_cost;
+    a.dSt = dSt;
+    a.k_T = k_T;
+    a.eta = eta;
+    a.iters = iters;
+    s = multi_run(h, a, static_cast<hipStream_t>(stream));
+    (void)hipSetDevice(h->device);
+    return s;
+}
+
+tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,
+                                   const double* seg_times, const double* end_derivs, double* coeffs,
+                                   int32_t* status) {
+    if (!h) return TGMS_ERR_INVALID_ARG;
+    if (!h->multi) return tgms_solve_batch(h, B, so, waypoints, seg_times, end_derivs, coeffs, status);
+    h->last_error.clear();
+    tgms_status s = check_offsets(h, B, so, max_m_for(h), nullptr, nullptr);
+    if (s != TGMS_OK || B == 0) return s;
+    if (!waypoints || !seg_times || !coeffs)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times/coeffs");
+    TGMS_HIP(h, hipSetDevice(h->device));
+    const size_t S = (size_t)so[B];
+    const size_t nW = (S + B) * 3, nT = S, nED = end_derivs ? (size_t)B * 18 : 0, nC = S * 24;
+    size_t off = 0;
+    const size_t oW = off; off = align256(off + nW * 8);
+    const size_t oT = off; off = align256(off + nT * 8);
+    const size_t oED = off; off = align256(off + nED * 8);
+    const size_t oC = off; off = align256(off + nC * 8);
+    const size_t oSt = off; off = align256(off + (size_t)B * 4);
+    const size_t oSo = off; off = align256(off + (size_t)(B + 1) * 4);
+    s = ensure_ws(h, off);
+    if (s != TGMS_OK) return s;
+    char* base = static_cast<char*>(h->d_ws);
+    double* dW = reinterpret_cast<double*>(base + oW);
+    double* dT = reinterpret_cast<double*>(base + oT);
+    double* dED = end_derivs ? reinterpret_cast<double*>(base + oED) : nullptr;
+    double* dC = reinterpret_cast<double*>(base + oC);
+    int32_t* dSt = reinterpret_cast<int32_t*>(base + oSt);
+    int32_t* dSo = reinterpret_cast<int32_t*>(base + oSo);
+    hipStream_t st = h->stream;
+    TGMS_HIP(h, hipMemcpyAsync(dW, waypoints, nW * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dT, seg_times, nT * 8, hipMemcpyHostToDevice, st));
+    if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
+    TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
+    MultiArgs a;
+    a.B = B;
+    a.h_so = so;
+    a.d_so = dSo;
+    a.dW = dW;
+    a.dT = dT;
+    a.dED = dED;
+    a.dC = dC;
+    a.dSt = dSt;
+    s = multi_run(h, a, st);
+    (void)hipSetDevice(h->device);
+    if (s != TGMS_OK) return s;
+    TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> hst;
+    int32_t* stout = status;
+    if (!stout) {
+        hst.resize(B);
+        stout = hst.data();
+    }
+    TGMS_HIP(h, hipMemcpyAsync(stout, dSt, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    TGMS_HIP(h, hipStreamSynchronize(st));
+    return worst_status(h, stout, B);
 }
 
 }  // extern "C"

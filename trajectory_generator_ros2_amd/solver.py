@@ -30,14 +30,22 @@ def _ptr(a) -> Optional[int]:
 class Solver:
     """A libtgms handle bound to one HIP device."""
 
-    def __init__(self, device: int = 0, method: int = _lib.METHOD_REDUCED):
+    def __init__(self, device: int = 0, method: int = _lib.METHOD_REDUCED, device_count: int = 0):
+        """device_count > 0: a multi-GPU handle over devices 0..device_count-1
+        (tgms_create_multi: one RCCL communicator per device); else one device."""
         self._L = _lib.load()
         h = ctypes.c_void_p()
-        st = self._L.tgms_create(ctypes.byref(h), int(device))
+        if device_count > 0:
+            st = self._L.tgms_create_multi(ctypes.byref(h), int(device_count))
+            what = "tgms_create_multi"
+        else:
+            st = self._L.tgms_create(ctypes.byref(h), int(device))
+            what = "tgms_create"
         if st != _lib.OK:
-            raise TgmsError(st, "tgms_create failed (no CPU fallback exists)")
+            raise TgmsError(st, f"{what} failed (no CPU fallback exists)")
         self._h = h
-        self.device = device
+        self.device = 0 if device_count > 0 else device
+        self.device_count = int(self._L.tgms_device_count(h))
         self.set_method(method)
 
     def close(self):
@@ -90,6 +98,20 @@ class Solver:
             st = np.zeros(max(B, 1), dtype=np.int32)
         worst = self._L.tgms_solve_batch(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), _ptr(C), _ptr(st))
         if check and worst not in (_lib.OK,) and worst in (_lib.ERR_DEVICE, _lib.ERR_NO_DEVICE):
+            raise TgmsError(worst, self.last_error())
+        return C, st[:B], worst
+
+    def solve_multi(self, seg_offsets, waypoints, seg_times, end_derivs=None) -> Tuple[np.ndarray, np.ndarray, int]:
+        """tgms_solve_batch_multi: host batch over every device of the handle."""
+        so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+        W = np.ascontiguousarray(waypoints, dtype=np.float64).reshape(-1, 3)
+        T = np.ascontiguousarray(seg_times, dtype=np.float64).reshape(-1)
+        ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64).reshape(-1, 18)
+        B = so.shape[0] - 1
+        C = np.zeros((int(so[-1]) if B > 0 else 0, 3, 8), dtype=np.float64)
+        st = np.zeros(max(B, 1), dtype=np.int32)
+        worst = self._L.tgms_solve_batch_multi(self._h, B, _ptr(so), _ptr(W), _ptr(T), _ptr(ED), _ptr(C), _ptr(st))
+        if worst in (_lib.ERR_DEVICE, _lib.ERR_NO_DEVICE):
             raise TgmsError(worst, self.last_error())
         return C, st[:B], worst
 
@@ -175,6 +197,26 @@ class Solver:
         if st != _lib.OK:
             raise TgmsError(st, self.last_error())
 
+    def solve_batch_multi_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, d_coeffs,
+                                 d_status=None, d_end_derivs=None, stream: int = 0) -> None:
+        so = np.ascontiguousarray(h_seg_offsets, dtype=np.int32)
+        st = self._L.tgms_solve_batch_multi_device(self._h, int(so.shape[0] - 1), _ptr(so), _ptr(d_seg_offsets),
+                                                   _ptr(d_waypoints), _ptr(d_seg_times), _ptr(d_end_derivs),
+                                                   _ptr(d_coeffs), _ptr(d_status), ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
+    def refine_loop_multi_device(self, h_seg_offsets, d_seg_offsets, d_waypoints, d_seg_times, k_T: float,
+                                 eta: float, iters: int, d_coeffs=None, d_cost=None, d_status=None,
+                                 d_end_derivs=None, stream: int = 0) -> None:
+        so = np.ascontiguousarray(h_seg_offsets, dtype=np.int32)
+        st = self._L.tgms_refine_loop_multi_device(self._h, int(so.shape[0] - 1), _ptr(so), _ptr(d_seg_offsets),
+                                                   _ptr(d_waypoints), _ptr(d_seg_times), _ptr(d_end_derivs),
+                                                   float(k_T), float(eta), int(iters), _ptr(d_coeffs),
+                                                   _ptr(d_cost), _ptr(d_status), ctypes.c_void_p(stream))
+        if st != _lib.OK:
+            raise TgmsError(st, self.last_error())
+
     def sample_device(self, B: int, d_seg_offsets, d_waypoints, d_seg_times, d_coeffs, dt: float,
                       d_sample_offsets, d_out, d_end_derivs=None, yaw_mode: int = _lib.YAW_CONSTANT,
                       yaw_const: float = 0.0, stream: int = 0) -> None:
@@ -199,3 +241,13 @@ def sample_offsets(seg_offsets, seg_times, dt: float) -> np.ndarray:
     if st != _lib.OK:
         raise TgmsError(st, "tgms_sample_offsets")
     return offs
+
+
+def plan_shards(seg_offsets, parts: int, method: int = _lib.METHOD_REDUCED) -> np.ndarray:
+    """tgms_plan_shards (host only): [parts+1] contiguous cost-balanced trajectory bounds."""
+    so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+    bounds = np.zeros(int(parts) + 1, dtype=np.int32)
+    st = _lib.load().tgms_plan_shards(int(so.shape[0] - 1), _ptr(so), int(parts), int(method), _ptr(bounds))
+    if st != _lib.OK:
+        raise TgmsError(st, "tgms_plan_shards")
+    return bounds
