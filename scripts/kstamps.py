@@ -20,7 +20,8 @@ for _ in range(20):
     s.solve_uniform_device(B, M, dW, dT, dC, dS)
 torch.cuda.synchronize()
 L = _lib.load()
-nw = (B + 31) // 32
+TPW = int(os.environ.get("KB_TPW", 64))  # trajectories per wave of the stamped kernel
+nw = (B + TPW - 1) // TPW
 buf = (ctypes.c_ulonglong * (nw * 16))()
 L.tgms_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 assert L.tgms_debug_stamps(buf, nw * 16)
@@ -32,7 +33,8 @@ clk = (st[:, 5] - st[:, 0]).sum() / max(((rt[:, 1] - rt[:, 0]) * 10).sum(), 1)  
 xcc = st[:, 8] & 0xF
 hw = st[:, 9]
 ph = np.diff(st[:, :6], axis=1)
-names = ["load+stage", "chain", "interface", "backsub", "emission"]
+names = (["stage_T", "factor", "stage_W", "forward", "back+emit"] if TPW == 64 else
+         ["load+stage", "chain", "interface", "backsub", "emission"])
 out = {"waves": int(nw), "clock_GHz": float(clk),
        "phase_us_mean": {n: float(ph[:, i].mean() / clk / 1e3) for i, n in enumerate(names)},
        "wave_life_us_mean": float((st[:, 5] - st[:, 0]).mean() / clk / 1e3)}

@@ -128,12 +128,12 @@ __device__ __forceinline__ LaneView make_view(const In<M>& sm, int slot, bool ri
 // [trajectory][knot][axis] and [trajectory][segment], copied 16 B per lane with no
 // index arithmetic; 1/T replaces T.  Column reads across the 32 slots are
 // conflict-free for W (66-dword stride) and at most 2-way for R (20-dword stride).
-template <int M>
+template <int M, int NT = TPW>
 struct RawIn {
     static constexpr int NW = (M + 1) * 3;
-    double W[TPW * NW];
-    double R[TPW * M];
-    int bad[TPW];
+    double W[NT * NW];
+    double R[NT * M];
+    int bad[NT];
 };
 
 template <int M>
@@ -857,11 +857,11 @@ __device__ __forceinline__ void sanitize(In<M>& sm, int lane) {
 // (which needs only 1/T) runs while the waypoints are still in flight.  Only a wave
 // that sees an invalid input builds per-trajectory flags (re-reading its rows from
 // HBM) and sanitises the bad trajectories (all-zero waypoints, unit times).
-template <int M>
+template <int M, int NT = TPW>
 struct RawLoader {
-    static constexpr int NW = RawIn<M>::NW;
-    static constexpr int NW2 = (TPW * NW / 2 + W64 - 1) / W64;  // double2 per lane, waypoints
-    static constexpr int NT2 = (TPW * M / 2 + W64 - 1) / W64;   // double2 per lane, times
+    static constexpr int NW = RawIn<M, NT>::NW;
+    static constexpr int NW2 = (NT * NW / 2 + W64 - 1) / W64;  // double2 per lane, waypoints
+    static constexpr int NT2 = (NT * M / 2 + W64 - 1) / W64;   // double2 per lane, times
     double2 wv[NW2], tv[NT2];
     double wl, tl;
     bool oddW, oddT, anyT;
@@ -896,9 +896,9 @@ struct RawLoader {
     }
 
     // Per-trajectory validity from HBM (rare path), sanitising the bad ones' times.
-    __device__ __forceinline__ void flags(RawIn<M>& sm, const double* __restrict__ W,
+    __device__ __forceinline__ void flags(RawIn<M, NT>& sm, const double* __restrict__ W,
                                           const double* __restrict__ T, int64_t b0, int nb, int lane) {
-        if (lane < TPW) {
+        if (lane < NT) {
             int f = 0;
             if (lane < nb) {
                 const double* w = W + (b0 + lane) * NW;
@@ -912,13 +912,13 @@ struct RawLoader {
         }
     }
 
-    __device__ __forceinline__ void stage_T(RawIn<M>& sm, const double* __restrict__ W,
+    __device__ __forceinline__ void stage_T(RawIn<M, NT>& sm, const double* __restrict__ W,
                                             const double* __restrict__ T, int64_t b0, int nb, int lane) {
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < NT2; ++i) {
             const int e = 2 * (lane + W64 * i);
-            if ((TPW * M) % (2 * W64) == 0 || e < TPW * M) {
+            if ((NT * M) % (2 * W64) == 0 || e < NT * M) {
                 *reinterpret_cast<double2*>(sm.R + e) = make_double2(fast_rcp(tv[i].x), fast_rcp(tv[i].y));
                 bad = bad || (e < nt && !finite_pos(tv[i].x)) || (e + 1 < nt && !finite_pos(tv[i].y));
             }
@@ -933,13 +933,13 @@ struct RawLoader {
     }
 
     // Returns (wave-uniform) whether any trajectory of the group is invalid.
-    __device__ __forceinline__ bool stage_W(RawIn<M>& sm, const double* __restrict__ W,
+    __device__ __forceinline__ bool stage_W(RawIn<M, NT>& sm, const double* __restrict__ W,
                                             const double* __restrict__ T, int64_t b0, int nb, int lane) {
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < NW2; ++i) {
             const int e = 2 * (lane + W64 * i);
-            if ((TPW * NW) % (2 * W64) == 0 || e < TPW * NW) {
+            if ((NT * NW) % (2 * W64) == 0 || e < NT * NW) {
                 *reinterpret_cast<double2*>(sm.W + e) = wv[i];
                 bad = bad || (e < nw && !finite(wv[i].x)) || (e + 1 < nw && !finite(wv[i].y));
             }
@@ -951,7 +951,7 @@ struct RawLoader {
         const bool anyW = __builtin_amdgcn_ballot_w64(bad) != 0;
         if (anyW && !anyT) flags(sm, W, T, b0, nb, lane);
         if (anyW || anyT) {
-            if (lane < TPW && sm.bad[lane])
+            if (lane < NT && sm.bad[lane])
                 for (int q = 0; q < NW; ++q) sm.W[lane * NW + q] = 0.0;
         }
         wave_lds_sync();
@@ -1385,12 +1385,505 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(Group
     }
 }
 
+// ---------------------------------------------------------------------------
+// Lane-per-trajectory solve of a uniform batch with an even number of segments
+// (configs 2-4: M = 10 is the headline).  One LANE owns one trajectory, 64 per
+// wavefront, one wavefront per SIMD: the 512-register budget holds the whole
+// elimination state (every knot's G = D^-1 C and g = D^-1 z, 3 axes) at once, so
+//   * the three axes are solved together — the shared powers, couplings and
+//     right-hand-side factors are computed once per knot instead of once per axis,
+//     and the three substitutions give the scheduler independent chains;
+//   * there is no twisted interface: the chain runs knot 1 .. M-1 in one lane;
+//   * every segment's 24 coefficients are final at the same moment, so the output
+//     leaves as WHOLE 128-B lines.  In the [traj][seg][axis][8] layout the segment
+//     pair (2k, 2k+1) is exactly three lines: (2k: x y), (2k: z | 2k+1: x),
+//     (2k+1: y z).  Back substitution runs from the last segment down, so segment
+//     2k+1 flushes its (y z) line and carries its x row until segment 2k completes
+//     the other two.  Each flush stages one line per lane in LDS and stores it with
+//     8 instructions of 8 whole lines each (half-line writes a pass apart, the
+//     axis-sequential kernel's pattern, run at ~3.4 TB/s past the Infinity Cache;
+//     whole lines at ~5.5, scripts/storebench.hip).
+// Inputs arrive by LDS-DMA (global_load_lds_dwordx4, lane-linear in the HBM layout,
+// no staging registers): the times first, so the factorisation (1/T only) runs while
+// the waypoints are still in flight.  1/T stays in LDS (each lane's row) and is
+// re-read per phase, which keeps the elimination state alone in registers.
+// Same block LDL^T as the oracle's reduced formulation (oracle/minsnap_oracle.c),
+// one-sided instead of twisted.
+
+// Anchor a value at this point of the instruction stream: it must be computed before
+// the (volatile, ordered) statement, so IR-level sinking cannot pile every knot's
+// arithmetic into one block after the last scheduling fence (which only orders the
+// machine scheduler): without the anchors the kernel needs > 700 registers.
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin33(double (&m)[3][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) pin(m[i][j]);
+}
+__device__ __forceinline__ void pin_ldl3(Ldl3& f) {
+    pin(f.i0);
+    pin(f.i1);
+    pin(f.i2);
+    pin(f.l10);
+    pin(f.l20);
+    pin(f.l21);
+}
+
+// LDS byte address of a __shared__ object.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// 16-B LDS-DMA (global_load_lds_dwordx4): lane l's 16 B from `src` land at LDS byte
+// lds + 16 l.  Issued as asm so the compiler's wait bookkeeping ignores it (with the
+// builtin it drains every copy, vmcnt(0), at the first LDS read of ANY object); the
+// kernel counts completion itself.
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+
+constexpr int LTPW = 64;   // trajectories per wavefront (one per lane)
+constexpr int LROW = 18;   // staged output line: 16 doubles padded to 144 B (conflict-free ds_*_b128)
+
+// LDS-DMA copies of one wave's input block (lane-linear, 1 KiB per instruction).
+template <int M>
+struct LaneDma {
+    static constexpr int NW = (M + 1) * 3;
+    static constexpr int NTI = (LTPW * M * 8 + 1023) / 1024;   // instructions, times
+    static constexpr int NWI = (LTPW * NW * 8 + 1023) / 1024;  // instructions, waypoints
+};
+
+struct LineOut {
+    double* stage[2];              // LDS [LTPW][LROW], alternating per flush
+    __amdgpu_buffer_rsrc_t rs[8];  // store q: trajectories 8q .. 8q+7 of the wave's block
+    uint32_t voff;                 // lane's 16-B piece: trajectory (lane >> 3) of the group, piece (lane & 7)
+    bool nt;                       // streaming stores (the batch's output exceeds the Infinity Cache)
+    int lane;
+};
+
+template <int M>
+__device__ __forceinline__ LineOut make_line_out(double* s0, double* s1, double* C, int64_t b0, int nb, int lane,
+                                                 bool nt) {
+    constexpr int TRAJ_B = M * 24 * 8;
+    LineOut o;
+    o.stage[0] = s0;
+    o.stage[1] = s1;
+    o.lane = lane;
+    o.nt = nt;
+    double* base = C + b0 * (M * 24);
+    const int block = nb * TRAJ_B;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int lim = block - q * 8 * TRAJ_B;
+        o.rs[q] = __builtin_amdgcn_make_buffer_rsrc(base + (int64_t)q * 8 * M * 24, (short)0, lim > 0 ? lim : 0,
+                                                    0x00020000);
+    }
+    o.voff = (uint32_t)((lane >> 3) * TRAJ_B + (lane & 7) * 16);
+    return o;
+}
+
+// Output lines are software-pipelined: a segment's lines are written to the stage
+// (one 128-B line per lane per buffer, lo = first 64 B, hi = second) and stored one
+// segment later, so the next segment's arithmetic covers the LDS write latency.
+// Storing reads a buffer transposed — 8 consecutive lanes hold one line — and writes
+// it with 8 instructions of 8 whole lines (the resources' range check drops a tail
+// wave's missing trajectories).  LDS operations of a wave execute in order, so a
+// buffer may be rewritten right after it was read.
+__device__ __forceinline__ void stage_line(const LineOut& o, int buf, const double (&lo)[8], const double (&hi)[8]) {
+    double2* d = reinterpret_cast<double2*>(o.stage[buf] + o.lane * LROW);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = make_double2(lo[2 * j], lo[2 * j + 1]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[4 + j] = make_double2(hi[2 * j], hi[2 * j + 1]);
+}
+
+struct StagedLine {
+    double2 v[8];
+};
+
+__device__ __forceinline__ void read_line(const LineOut& o, int buf, StagedLine& L) {
+    const double* src = o.stage[buf] + (o.lane >> 3) * LROW + (o.lane & 7) * 2;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) L.v[q] = *reinterpret_cast<const double2*>(src + q * 8 * LROW);
+}
+
+__device__ __forceinline__ void store_line(const LineOut& o, const StagedLine& L, int line_off) {
+#ifdef TGMS_ABL_NOSTORE  // ablation build (scripts/gpu_kvar.sh): the stores' data stays live, nothing is written
+#pragma unroll
+    for (int q = 0; q < 8; ++q) asm volatile("" ::"v"(L.v[q].x), "v"(L.v[q].y));
+    return;
+#endif
+    if (o.nt) {  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, L.v[q]), o.rs[q], o.voff, line_off,
+                                                   TGMS_STORE_CPOL_NT);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, L.v[q]), o.rs[q], o.voff, line_off,
+                                                   TGMS_STORE_CPOL);
+    }
+}
+
+// The lines segment e leaves staged (M even, descending order): an odd segment its
+// (y z) line in buffer 0, an even one (x y) in buffer 0 and (z | carry) in buffer 1.
+__device__ __forceinline__ int seg_lines(int e) { return (e & 1) ? 1 : 2; }
+__device__ __forceinline__ int seg_line_off(int e, int i) { return (e & 1) ? e * 192 + 64 : e * 192 + 128 * i; }
+
+// Store the lines segment e staged (called one segment later, after wave_lds_sync).
+__device__ __forceinline__ void put_segment_lines_read(const LineOut& o, int e, StagedLine& L0, StagedLine& L1) {
+    read_line(o, 0, L0);
+    if (seg_lines(e) == 2) read_line(o, 1, L1);
+}
+__device__ __forceinline__ void put_segment_lines_store(const LineOut& o, int e, const StagedLine& L0,
+                                                        const StagedLine& L1) {
+    store_line(o, L0, seg_line_off(e, 0));
+    if (seg_lines(e) == 2) store_line(o, L1, seg_line_off(e, 1));
+}
+
+// Monomial coefficients of segment e, all three axes, from the Hermite data at its
+// knots (xs at knot e, xe at knot e+1, [derivative][axis]) in r = 1/T scaled
+// variables (the same expressions as emit_axis).
+__device__ __forceinline__ void seg_rows(const double (&ws)[3], const double (&we)[3], double r,
+                                         const double (&xs)[3][3], const double (&xe)[3][3], double (&c)[3][8]) {
+    const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double w0 = ws[a], w1 = we[a];
+        const double v0 = xs[0][a], a0 = xs[1][a], j0 = xs[2][a];
+        const double v1 = xe[0][a], a1 = xe[1][a], j1 = xe[2][a];
+        const double D = (w1 - w0) * r3;
+        const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
+        const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
+        const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
+        const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
+        const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+        c[a][0] = w0;
+        c[a][1] = v0;
+        c[a][2] = 0.5 * a0;
+        c[a][3] = j0 * (1.0 / 6.0);
+        c[a][4] = P4 * r;
+        c[a][5] = P5 * r2;
+        c[a][6] = P6 * r3;
+        c[a][7] = P7 * r4;
+    }
+}
+
+// Emit segment e (descending order, M even): store the lines the segment above left
+// staged, then stage this segment's: an odd segment its (y z) line, keeping its x row
+// in `carry`; the even segment below it (x y) and (z | carry).
+__device__ __forceinline__ void emit_lane_segment(const LineOut& o, const double (&ws)[3], const double (&we)[3],
+                                                  double r, int e, const double (&xs)[3][3],
+                                                  const double (&xe)[3][3], double (&carry)[8], int e_prev) {
+    double c[3][8];
+    seg_rows(ws, we, r, xs, xe, c);
+    StagedLine L0, L1;
+    if (e_prev >= 0) {
+        wave_lds_sync();  // the previous segment's stage writes have landed
+        put_segment_lines_read(o, e_prev, L0, L1);
+    }
+    if (e & 1) {
+        stage_line(o, 0, c[1], c[2]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) carry[j] = c[0][j];
+    } else {
+        stage_line(o, 0, c[0], c[1]);
+        stage_line(o, 1, c[2], carry);
+    }
+    if (e_prev >= 0) put_segment_lines_store(o, e_prev, L0, L1);
+}
+
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double* __restrict__ W,
+                                                         const double* __restrict__ T,
+                                                         const double* __restrict__ ED, double* __restrict__ C,
+                                                         int32_t* __restrict__ status, int nt) {
+    static_assert(M >= 2 && M % 2 == 0, "segment pairs make whole lines only for even M");
+    using DM = LaneDma<M>;
+    constexpr int NK = M - 1;  // interior knots 1 .. M-1 (index k-1 below)
+    constexpr int NW = DM::NW;
+    __shared__ alignas(16) double sT[DM::NTI * 128];
+    __shared__ alignas(16) double sW[DM::NWI * 128];
+    __shared__ alignas(16) double sO[2][LTPW * LROW];
+    STAMP_RT(6);
+    STAMP(0);
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * LTPW;
+    const int nb = (int)((B - b0) < LTPW ? (B - b0) : LTPW);
+    const bool live = lane < nb;
+    const int64_t b = b0 + lane;
+    {
+        // 16-B pieces of the wave's block, indices clamped into the arrays (a tail
+        // wave copies junk for its missing trajectories; their results are dropped)
+        const int64_t nT2 = (int64_t)B * M / 2, nW2 = (int64_t)B * NW / 2;
+        const int64_t jT = b0 * M / 2, jW = b0 * NW / 2;  // b0 is a multiple of 64
+        const double2* gT = reinterpret_cast<const double2*>(T);
+        const double2* gW = reinterpret_cast<const double2*>(W);
+        const uint32_t aT = lds_addr(sT), aW = lds_addr(sW);
+#pragma unroll
+        for (int i = 0; i < DM::NTI; ++i) {
+            const int64_t j = jT + lane + W64 * i;
+            glds16(gT + (j < nT2 ? j : nT2 - 1), aT + i * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < DM::NWI; ++i) {
+            const int64_t j = jW + lane + W64 * i;
+            glds16(gW + (j < nW2 ? j : nW2 - 1), aW + i * 1024);
+        }
+    }
+    // the times' copies retire before the waypoints' (in order)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DM::NWI) : "memory");
+    double* __restrict__ Rl = sT + lane * M;  // this lane's row: T, then 1/T in place
+    bool valid = true;
+    {
+        double t[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            t[i] = Rl[i];
+            valid = valid && finite_pos(t[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < M; ++i) Rl[i] = valid ? fast_rcp(t[i]) : 1.0;  // invalid: unit times
+    }
+    wave_lds_sync();
+    STAMP(1);
+
+    // ---- block LDL^T over the interior knots (needs 1/T only) ----
+    // D_k = H_kk - C_{k-1}^T D_{k-1}^-1 C_{k-1};  G_{k-1} = D_{k-1}^-1 C_{k-1}
+    Ldl3 F[NK];
+    double G[NK > 1 ? NK - 1 : 1][3][3];
+    bool spd = true;
+    {
+        double pp[8];
+        rpowers(Rl[0], pp);
+#pragma unroll
+        for (int k = 1; k <= NK; ++k) {
+            SCHED_FENCE();
+            double pn[8];
+            rpowers(Rl[k], pn);
+            Sym3 D = knot_diag(pp, pn);
+            if (k >= 2) {
+                double Bc[3][3];
+                coupling(pp, Bc);  // C_{k-1} = H_{k-1, k}
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                    ldl3_solve(F[k - 2], Bc[0][e], Bc[1][e], Bc[2][e], G[k - 2][0][e], G[k - 2][1][e], G[k - 2][2][e]);
+                sym_sub_btw(D, Bc, G[k - 2]);
+            }
+            bool ok;
+            F[k - 1] = ldl3s(D, ok);
+            spd = spd && ok;
+            pin_ldl3(F[k - 1]);
+            if (k >= 2) pin33(G[k - 2]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+        }
+    }
+    STAMP(2);
+
+    // ---- waypoints (in flight until now) ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((((int64_t)B * NW) & 1) && b0 + nb == B) {  // the array's last double is in no 16-B piece
+        if (lane == 0) sW[nb * NW - 1] = W[(int64_t)B * NW - 1];
+        wave_lds_sync();
+    }
+    double* __restrict__ Wl = sW + lane * NW;
+    STAMP(3);
+    double u0[3][3], uM[3][3];  // end derivatives [derivative][axis]
+    {
+        const double* ed = ED + (live ? b : 0) * 18;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                u0[d][a] = HAS_ED ? ed[d * 3 + a] : 0.0;
+                uM[d][a] = HAS_ED ? ed[9 + d * 3 + a] : 0.0;
+            }
+    }
+
+    // ---- forward substitution, 3 axes: z_k = y_k - G_{k-1}^T z_{k-1}, g_k = D_k^-1 z_k ----
+    double g[NK][3][3];
+    bool wfin = true;
+    {
+        double pp[8], zp[3][3];
+        rpowers(Rl[0], pp);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) wfin = wfin && finite(Wl[a]) && finite(Wl[3 + a]);
+#pragma unroll
+        for (int k = 1; k <= NK; ++k) {
+            SCHED_FENCE();
+            double pn[8];
+            rpowers(Rl[k], pn);
+            const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
+            const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+            double z[3][3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double wk = Wl[k * 3 + a];
+                const double wn = Wl[(k + 1) * 3 + a];
+                wfin = wfin && finite(wn);
+                const double dp = wk - Wl[(k - 1) * 3 + a];
+                const double dn = wn - wk;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) z[d][a] = fp[d] * dp + fn[d] * dn;
+            }
+            if (HAS_ED && k == 1) {  // - C_0^T u0
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) {
+                        const double c0 = KSE[e][d] * pp[5 - d - e];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) z[d][a] -= c0 * u0[e][a];
+                    }
+            }
+            if (HAS_ED && k == NK) {  // - C_{M-1} uM
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) {
+                        const double c1 = KSE[d][e] * pn[5 - d - e];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) z[d][a] -= c1 * uM[e][a];
+                    }
+            }
+            if (k >= 2) {
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        z[d][a] -= G[k - 2][0][d] * zp[0][a] + G[k - 2][1][d] * zp[1][a] + G[k - 2][2][d] * zp[2][a];
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                ldl3_solve(F[k - 1], z[0][a], z[1][a], z[2][a], g[k - 1][0][a], g[k - 1][1][a], g[k - 1][2][a]);
+            pin33(g[k - 1]);
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) zp[d][a] = z[d][a];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+        }
+    }
+    if (HAS_ED) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) wfin = wfin && finite(u0[d][a]) && finite(uM[d][a]);
+    }
+    // An invalid trajectory (non-finite input, T <= 0) comes out as exact zeros: its
+    // elimination vectors, end derivatives and waypoint row are zeroed (rare path).
+    valid = valid && wfin;
+    if (__builtin_amdgcn_ballot_w64(!valid) != 0) {
+        if (!valid) {
+#pragma unroll
+            for (int q = 0; q < NW; ++q) Wl[q] = 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) g[k][d][a] = valid ? g[k][d][a] : 0.0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                u0[d][a] = valid ? u0[d][a] : 0.0;
+                uM[d][a] = valid ? uM[d][a] : 0.0;
+            }
+        wave_lds_sync();
+    }
+    STAMP(4);
+
+    // ---- back substitution x_k = g_k - G_k x_{k+1}, each segment emitted as soon as
+    // both of its knots are final (last segment first); the next segment's waypoints
+    // and 1/T are read one segment ahead ----
+    const LineOut O = make_line_out<M>(sO[0], sO[1], C, b0, nb, lane, nt != 0);
+    double carry[8];
+    double fin = 0.0;
+    double we[3], ws[3], rs = Rl[NK];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        we[a] = Wl[M * 3 + a];
+        ws[a] = Wl[NK * 3 + a];
+    }
+#pragma unroll
+    for (int k = NK; k >= 1; --k) {
+        SCHED_FENCE();
+        double wn[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) wn[a] = Wl[(k - 1) * 3 + a];
+        const double rn = Rl[k - 1];
+        if (k < NK) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    g[k - 1][d][a] -= G[k - 1][d][0] * g[k][0][a] + G[k - 1][d][1] * g[k][1][a] + G[k - 1][d][2] * g[k][2][a];
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) fin += (g[k - 1][d][0] + g[k - 1][d][1]) + g[k - 1][d][2];
+        if (k == NK)
+            emit_lane_segment(O, ws, we, rs, k, g[k - 1], uM, carry, -1);
+        else
+            emit_lane_segment(O, ws, we, rs, k, g[k - 1], g[k], carry, k + 1);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            we[a] = ws[a];
+            ws[a] = wn[a];
+        }
+        rs = rn;
+    }
+    SCHED_FENCE();
+    emit_lane_segment(O, ws, we, rs, 0, u0, g[0], carry, 1);
+    {
+        StagedLine L0, L1;
+        wave_lds_sync();
+        put_segment_lines_read(O, 0, L0, L1);
+        put_segment_lines_store(O, 0, L0, L1);
+    }
+    STAMP(5);
+    STAMP_RT(7);
+    int32_t st = TGMS_OK;
+    if (!valid)
+        st = TGMS_ERR_INVALID_ARG;
+    else if (!spd)
+        st = TGMS_ERR_SINGULAR;
+    else if (!finite(fin))
+        st = TGMS_ERR_NONFINITE;
+    if (live && status) status[b] = st;
+}
+
+// Uniform batches with an even number of segments take the lane-per-trajectory kernel.
+#ifndef TGMS_LANE_UNIFORM
+#define TGMS_LANE_UNIFORM 1
+#endif
+template <int M>
+constexpr bool use_lane_kernel() {
+    return TGMS_LANE_UNIFORM && M >= 2 && M % 2 == 0;
+}
+
 template <int M>
 hipError_t uniform_M(int32_t B, const double* W, const double* T, const double* ED, double* C, int32_t* status,
                      hipStream_t stream) {
     const unsigned grid = (unsigned)((B + TPW - 1) / TPW);
     if (grid == 0) return hipSuccess;
     const int nt = (int64_t)B * M * 24 * 8 > kStreamingOutputBytes;
+    if constexpr (use_lane_kernel<M>()) {
+        const unsigned lgrid = (unsigned)((B + LTPW - 1) / LTPW);
+        if (ED)
+            TGMS_LAUNCH((k_lane_uniform<M, true>), dim3(lgrid), dim3(W64), 0, stream, B, W, T, ED, C, status, nt);
+        else
+            TGMS_LAUNCH((k_lane_uniform<M, false>), dim3(lgrid), dim3(W64), 0, stream, B, W, T, ED, C, status, nt);
+        return hipSuccess;
+    }
     if (ED)
         TGMS_LAUNCH((k_reduced_uniform<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
                            nt);
