@@ -639,7 +639,8 @@ def main():
                          "traffic_source": (f"{TRAFFIC_FILE}[{key}]: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                             f"passes of this command (scripts/gpu_profile.sh), not this run")
                          if traffic is not None else None,
-                         "kernel": f"k_reduced_uniform<{M}>" if args.method == "reduced" else f"k_dense_kkt<{M}>",
+                         "kernel": (f"k_dense_kkt<{M}>" if args.method == "dense" else
+                                    f"k_lane_uniform<{M}>" if M % 2 == 0 else f"k_reduced_uniform<{M}>"),
                          "launch_ms": launch_ms_max,
                          "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
                          "algorithmic_bytes_per_launch": bpl},

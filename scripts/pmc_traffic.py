@@ -31,7 +31,11 @@ def per_dispatch(pmc_dir, kernel_substr):
 def main():
     pmc_dir = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
     key = sys.argv[2] if len(sys.argv) > 2 else "B65536_M10_reduced_sets4"
-    kernel = "k_reduced_uniform" if "reduced" in key else "k_dense_kkt"
+    if "reduced" in key:  # uniform even M: the lane-per-trajectory kernel; odd M: the lane-pair one
+        M = int(key.split("_M")[1].split("_")[0])
+        kernel = "k_lane_uniform" if M % 2 == 0 else "k_reduced_uniform"
+    else:
+        kernel = "k_dense_kkt"
     mean, n = per_dispatch(pmc_dir, kernel)
     if "FETCH_SIZE" not in mean or "WRITE_SIZE" not in mean:
         sys.exit(f"no FETCH_SIZE/WRITE_SIZE for {kernel} under {pmc_dir}")
