@@ -1659,13 +1659,14 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
     double G[NK > 1 ? NK - 1 : 1][3][3];
     bool spd = true;
     {
-        double pp[8];
+        double pp[8], rk = Rl[1];
         rpowers(Rl[0], pp);
 #pragma unroll
         for (int k = 1; k <= NK; ++k) {
             SCHED_FENCE();
             double pn[8];
-            rpowers(Rl[k], pn);
+            rpowers(rk, pn);
+            if (k < NK) rk = Rl[k + 1];  // LDS read one step ahead
             Sym3 D = knot_diag(pp, pn);
             if (k >= 2) {
                 double Bc[3][3];
@@ -1710,27 +1711,39 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
     double g[NK][3][3];
     bool wfin = true;
     {
-        double pp[8], zp[3][3];
+        // the waypoints of knots k-1, k, k+1 and 1/T of segment k, each read from LDS one
+        // step before it is needed
+        double pp[8], zp[3][3], wm[3], wc[3], wn[3], rk = Rl[1];
         rpowers(Rl[0], pp);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) wfin = wfin && finite(Wl[a]) && finite(Wl[3 + a]);
+        for (int a = 0; a < 3; ++a) {
+            wm[a] = Wl[a];
+            wc[a] = Wl[3 + a];
+            wn[a] = Wl[6 + a];
+            wfin = wfin && finite(wm[a]) && finite(wc[a]);
+        }
 #pragma unroll
         for (int k = 1; k <= NK; ++k) {
             SCHED_FENCE();
             double pn[8];
-            rpowers(Rl[k], pn);
+            rpowers(rk, pn);
+            double wnn[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) wnn[a] = (k < NK) ? Wl[(k + 2) * 3 + a] : 0.0;
+            if (k < NK) rk = Rl[k + 1];
             const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
             const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
             double z[3][3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double wk = Wl[k * 3 + a];
-                const double wn = Wl[(k + 1) * 3 + a];
-                wfin = wfin && finite(wn);
-                const double dp = wk - Wl[(k - 1) * 3 + a];
-                const double dn = wn - wk;
+                wfin = wfin && finite(wn[a]);
+                const double dp = wc[a] - wm[a];
+                const double dn = wn[a] - wc[a];
 #pragma unroll
                 for (int d = 0; d < 3; ++d) z[d][a] = fp[d] * dp + fn[d] * dn;
+                wm[a] = wc[a];
+                wc[a] = wn[a];
+                wn[a] = wnn[a];
             }
             if (HAS_ED && k == 1) {  // - C_0^T u0
 #pragma unroll
