@@ -345,3 +345,39 @@ def test_device_slices_and_alignment(solver):
     with pytest.raises(TgmsError) as e:
         solver.solve_uniform_device(100, M, odd, dT[:100], full[:100])
     assert e.value.status == ERR_INVALID_ARG and "aligned" in solver.last_error()
+
+
+@pytest.mark.parametrize("M", [2, 4, 10, 16])
+def test_lane_kernel_end_derivs_invalid_and_tail(solver, oracle, M):
+    """The lane-per-trajectory kernel (uniform batches, even M): end derivatives, a
+    partial last wavefront (B = 3 x 64 + 5) whose waypoint array has an odd number of
+    doubles (the last one outside every 16-B LDS-DMA piece), and invalid trajectories
+    in several wavefronts — T <= 0, non-finite T, a NaN waypoint, a NaN end derivative.
+    Valid trajectories match the oracle; invalid ones are flagged and come out as
+    exact zeros."""
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG
+    B = 3 * 64 + 5
+    so, W, T = _uniform(B, M, seed=900 + M)
+    assert (W.size % 2) == 1
+    rng = np.random.default_rng(900 + M)
+    ED = rng.normal(size=(B, 18))
+    T = T.copy(); W = W.copy()
+    T[3 * M + M - 1] = 0.0            # trajectory 3: T <= 0 (its last segment)
+    T[70 * M] = np.inf                # trajectory 70
+    W[130 * (M + 1) + M, 2] = np.nan  # trajectory 130: NaN at its last knot
+    ED[B - 1, 17] = np.nan            # last trajectory (tail wavefront): NaN end derivative
+    bad = [3, 70, 130, B - 1]
+    C, st, worst = solver.solve(so, W, T, ED)
+    assert worst == ERR_INVALID_ARG
+    assert all(st[b] == ERR_INVALID_ARG for b in bad)
+    good = np.setdiff1d(np.arange(B), bad)
+    assert (st[good] == 0).all()
+    Cb = C.reshape(B, M, 3, 8)
+    assert all((Cb[b] == 0.0).all() for b in bad)
+    R, rst = oracle.solve_batch(so, W, np.where(np.isfinite(T) & (T > 0), T, 1.0),
+                                np.nan_to_num(ED), oracle.REDUCED)
+    Rb = R.reshape(B, M, 3, 8)
+    for b in good:
+        for a in range(3):
+            ref = Rb[b, :, a]
+            assert np.abs(Cb[b, :, a] - ref).max() <= TOL * max(np.abs(ref).max(), 1e-300)
