@@ -1,6 +1,8 @@
 """Shared fixtures.  `-m gpu` tests need a HIP device and go through libtgms's C ABI;
 everything else runs on CPU (oracle vs goldens, host logic, ABI exports, gloo)."""
 import os
+
+os.environ.setdefault("TGMS_NODE_QUIET", "1")  # the node adapter logs every generation (as the reference does)
 import sys
 
 import numpy as np

@@ -9,7 +9,7 @@
 // in this image:
 //   snapstack_msgs2::msg::Goal  -> trajectory_generator::Goal   (Goal.hpp, same fields)
 //   rclcpp::Clock::SharedPtr    -> trajectory_generator::ClockPtr (steady clock)
-//   RCLCPP_INFO / RCLCPP_ERROR  -> log_info / log_error (stderr)
+//   RCLCPP_INFO / RCLCPP_ERROR  -> log_info / log_error (stderr; rclcpp logger under TGMS_ROS2)
 // With TGMS_ROS2 defined the real ROS types are used instead;
 // that configuration needs a ROS 2 workspace and is not built here.
 #pragma once
@@ -93,23 +93,37 @@ protected:
 
 namespace trajectory_generator {
 
-// RCLCPP_INFO / RCLCPP_ERROR stand-ins with the same printf-style formatting.
-inline void log_msg(const char* level, const char* fmt, va_list ap) {
-    std::fprintf(stderr, "[%s] [trajectory_generator]: ", level);
+// RCLCPP_INFO / RCLCPP_ERROR with the reference's printf-style formatting: through the
+// node's rclcpp logger when built into the node (TGMS_ROS2), else to stderr.  Info
+// lines are always emitted, as the reference logs "Time to calculate the traj" on every
+// generation (Line.cpp:87-88); TGMS_NODE_QUIET silences them outside ROS (test runs).
+inline void log_msg(bool error, const char* fmt, va_list ap) {
+#ifdef TGMS_ROS2
+    char buf[512];
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    if (error)
+        RCLCPP_ERROR(rclcpp::get_logger("trajectory_generator"), "%s", buf);
+    else
+        RCLCPP_INFO(rclcpp::get_logger("trajectory_generator"), "%s", buf);
+#else
+    std::fprintf(stderr, "[%s] [trajectory_generator]: ", error ? "ERROR" : "INFO");
     std::vfprintf(stderr, fmt, ap);
     std::fputc('\n', stderr);
+#endif
 }
 inline void log_info(const char* fmt, ...) {
-    if (!std::getenv("TGMS_NODE_VERBOSE")) return;
+#ifndef TGMS_ROS2
+    if (std::getenv("TGMS_NODE_QUIET")) return;
+#endif
     va_list ap;
     va_start(ap, fmt);
-    log_msg("INFO", fmt, ap);
+    log_msg(false, fmt, ap);
     va_end(ap);
 }
 inline void log_error(const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
-    log_msg("ERROR", fmt, ap);
+    log_msg(true, fmt, ap);
     va_end(ap);
 }
 
