@@ -1494,6 +1494,11 @@ __device__ __forceinline__ LineOut make_line_out(double* s0, double* s1, double*
 // wave's missing trajectories).  LDS operations of a wave execute in order, so a
 // buffer may be rewritten right after it was read.
 __device__ __forceinline__ void stage_line(const LineOut& o, int buf, const double (&lo)[8], const double (&hi)[8]) {
+#ifdef TGMS_ABL_NOSTAGE  // ablation build: the line's data stays live, no LDS traffic
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(lo[j]), "v"(hi[j]));
+    return;
+#endif
     double2* d = reinterpret_cast<double2*>(o.stage[buf] + o.lane * LROW);
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] = make_double2(lo[2 * j], lo[2 * j + 1]);
@@ -1506,6 +1511,11 @@ struct StagedLine {
 };
 
 __device__ __forceinline__ void read_line(const LineOut& o, int buf, StagedLine& L) {
+#ifdef TGMS_ABL_NOSTAGE
+#pragma unroll
+    for (int q = 0; q < 8; ++q) L.v[q] = make_double2((double)buf, (double)q);
+    return;
+#endif
     const double* src = o.stage[buf] + (o.lane >> 3) * LROW + (o.lane & 7) * 2;
 #pragma unroll
     for (int q = 0; q < 8; ++q) L.v[q] = *reinterpret_cast<const double2*>(src + q * 8 * LROW);
@@ -1581,7 +1591,14 @@ __device__ __forceinline__ void emit_lane_segment(const LineOut& o, const double
                                                   double r, int e, const double (&xs)[3][3],
                                                   const double (&xe)[3][3], double (&carry)[8], int e_prev) {
     double c[3][8];
+#ifdef TGMS_ABL_NOEMIT  // ablation build: no coefficient arithmetic (the knot data stays live)
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[a][j] = (j < 3) ? xs[j][a] : ((j < 6) ? xe[j - 3][a] : ws[a] + r);
+#else
     seg_rows(ws, we, r, xs, xe, c);
+#endif
     StagedLine L0, L1;
     if (e_prev >= 0) {
         wave_lds_sync();  // the previous segment's stage writes have landed
