@@ -262,7 +262,9 @@ def config4_line(solver, M, dev, stream, world, rank, B=131072, chunks=8, reps=3
             torch.cuda.synchronize()
             assert torch.equal(chk, out[r, :n]), f"gathered shard of rank {r} differs"
     gathered = (world - 1) * B * M * 24 * 8
-    line["gather"] = {"collective": "torch.distributed.gather (RCCL send/recv) per piece, overlapped with the solve",
+    backend = dist.get_backend()
+    line["gather"] = {"collective": f"torch.distributed.gather per piece, overlapped with the solve (backend {backend}"
+                                    + (": RCCL send/recv)" if backend == "nccl" else ")"),
                       "pieces": chunks, "ms_total": ms, "trajectories_per_s": world * B / (ms * 1e-3),
                       "bytes_into_rank0": gathered, "rank0_ingest_GBs": gathered / (ms * 1e-3) / 1e9}
     return line
@@ -395,6 +397,9 @@ def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl",
+                    help="process-group backend at N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 control "
+                         "flow with several ranks on one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
@@ -425,8 +430,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % max(torch.cuda.device_count(), 1) if args.backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
 
