@@ -54,7 +54,7 @@ extern "C" {
 
 #define TGMS_ABI_VERSION 1
 #define TGMS_MAX_SEGMENTS 16       /* reduced-Hessian kernel: M = 1..16 (config 5 range) */
-#define TGMS_DENSE_MAX_SEGMENTS 10 /* dense KKT kernel: N = 14M+2 <= 142 fits 160 KiB LDS */
+#define TGMS_DENSE_MAX_SEGMENTS 10 /* dense KKT kernel: N = 14M+2 <= 142 (+3 right-hand sides) fits a 256-thread workgroup's registers */
 #define TGMS_GOAL_STRIDE 14        /* doubles per sample: p[3] v[3] a[3] j[3] psi dpsi */
 
 typedef enum tgms_status {

@@ -8,12 +8,14 @@ import torch
 from trajectory_generator_ros2_amd.solver import Solver
 from trajectory_generator_ros2_amd import synthetic as S
 
-B = int(os.environ.get("KB_B", 65536)); M = int(os.environ.get("KB_M", 10)); K = 30
+B = int(os.environ.get("KB_B", 65536)); M = int(os.environ.get("KB_M", 10)); K = int(os.environ.get("KB_K", 30))
+METHOD = int(os.environ.get("KB_METHOD", 0))  # 0 reduced, 1 dense KKT, 2 band KKT
 so, W, T = S.uniform_batch(B, M)
 dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
 dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
 dS = torch.empty((B,), dtype=torch.int32, device="cuda")
 s = Solver(0)
+s.set_method(METHOD)
 sp = torch.cuda.current_stream().cuda_stream
 for _ in range(3):
     s.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
@@ -48,6 +50,7 @@ if len(bad):
     print(json.dumps({"n_bad": int(len(bad)), "first_bad": bad[:8].tolist(),
                       "worst": np.unravel_index(int(errs.argmax()), errs.shape)[0].item()}), file=sys.stderr)
 print(json.dumps({"lib": os.path.basename(os.environ.get("TGMS_LIB", "default")), "B": B, "M": M, "rot": ROT,
+                  "method": METHOD,
                   "median_us": ms[K // 2] * 1e3, "min_us": ms[0] * 1e3,
                   "traj_per_s": B / (ms[K // 2] * 1e-3), "max_rel_err": err,
                   "status_ok": bool((dS == 0).all().item())}))
