@@ -16,7 +16,7 @@ if [ -d gpurun_out/pmc ]; then
 import json, sys
 d = json.load(open("profiles/pmc_traffic.json"))["B65536_M10_reduced_sets4"]
 with open(f"profiles/{sys.argv[1]}_pmc_summary.txt", "w") as f:
-    f.write("k_reduced_uniform, headline bench (fresh batch every launch), mean per dispatch\n")
+    f.write(f"{d['kernel']}, headline bench (fresh batch every launch), mean per dispatch\n")
     f.write(f"HBM bytes/launch (FETCH_SIZE x2 + WRITE_SIZE): {d['hbm_bytes_per_launch']:.0f}\n")
     for k, v in sorted(d["other_counters"].items()):
         f.write(f"{k:28s} {v:16.1f}\n")
