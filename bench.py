@@ -270,6 +270,31 @@ def config4_line(solver, M, dev, stream, world, rank, B=131072, chunks=8, reps=3
     return line
 
 
+def launch_stats(solver, B, M, bufs, stream, warm=3, n=25):
+    """SURVEY.md §8(d) timing method, kernel only: `warm` untimed launches, then `n`
+    launches each bracketed by its own pair of HIP events on the launch stream, a fresh
+    batch every launch (the sets rotated as in the headline); median and spread."""
+    import torch
+    sp = stream.cuda_stream
+    sets = len(bufs)
+    for k in range(warm):
+        dW, dT, dC, dS = bufs[k % sets]
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for k in range(n):
+        dW, dT, dC, dS = bufs[(warm + k) % sets]
+        ev[k][0].record(stream)
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    us = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+    q = lambda f: us[min(n - 1, int(f * n))]
+    return {"launches": n, "warmup": warm, "median_us": q(0.5), "p10_us": q(0.1), "p90_us": q(0.9),
+            "min_us": us[0], "max_us": us[-1],
+            "median_GBs": algorithmic_bytes_per_traj(M) * B / (q(0.5) * 1e-6) / 1e9,
+            "how": "one HIP event pair per launch on the launch stream, a fresh batch every launch"}
+
+
 def cache_resident_line(solver, B, M, buf, stream, K=40):
     """The same launch re-solving ONE batch K times: its 148.6 MB (inputs + output)
     stay in the 256 MiB Infinity Cache between launches, so the coefficient stores
@@ -337,14 +362,15 @@ def node_line(reps=20):
             "cpu_oracle_ms_solve_and_sample": sorted(tc)[reps // 2] * 1e3}
 
 
-def host_line(solver, B, M, W, T, reps=3):
+def host_line(solver, B, M, W, T, reps=20):
     """PCIe-inclusive rate: tgms_solve_batch on host buffers (H2D, solve, D2H), the call
     the node makes; reported beside `value`, never as it (SURVEY.md 8(d) timing)."""
     import numpy as np
     so = (np.arange(B + 1, dtype=np.int32) * M)
     Wf, Tf = W.reshape(-1, 3), T.reshape(-1)
     out = (np.zeros((B * M, 3, 8)), np.zeros(B, dtype=np.int32))  # caller-owned, reused
-    C, st, worst = solver.solve(so, Wf, Tf, out=out)  # warm-up (workspace, page faults)
+    for _ in range(3):  # warm-up (workspace, page faults)
+        C, st, worst = solver.solve(so, Wf, Tf, out=out)
     assert worst == 0, worst
     ts = []
     for _ in range(reps):
@@ -353,9 +379,11 @@ def host_line(solver, B, M, W, T, reps=3):
         ts.append(time.perf_counter() - t0)
     ms = sorted(ts)[len(ts) // 2] * 1e3
     nbytes = algorithmic_bytes_per_traj(M) * B + (B + 1) * 4
-    return {"trajectories": B, "ms_per_call": ms, "trajectories_per_s": B / (ms * 1e-3),
+    return {"trajectories": B, "ms_per_call": ms, "ms_min": sorted(ts)[0] * 1e3, "calls": reps, "warmup": 3,
+            "trajectories_per_s": B / (ms * 1e-3),
             "pcie_bytes": nbytes, "effective_GBs": nbytes / (ms * 1e-3) / 1e9,
-            "path": "tgms_solve_batch, pageable host numpy buffers reused across calls"}
+            "path": "tgms_solve_batch (end to end: H2D, solve, D2H), pageable host numpy buffers reused across "
+                    "calls; median of the calls"}
 
 
 def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
@@ -537,6 +565,7 @@ def main():
     launch_mode = "hip_graph_of_K_steps" if graph is not None else "python_loop"
     del graph
 
+    per_launch = launch_stats(solver, B, M, bufs, stream)
     cache_res = None
     if args.cache_resident and args.method == "reduced":
         cache_res = cache_resident_line(solver, B, M, bufs[0], stream)
@@ -654,6 +683,7 @@ def main():
                          "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
                          "algorithmic_bytes_per_launch": bpl},
             "cpu_baseline": cpu,
+            "per_launch": per_launch,
             "cache_resident": cache_res,
             "dense_kkt": dense,
             "band_kkt": band,
