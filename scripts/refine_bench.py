@@ -10,8 +10,9 @@ from trajectory_generator_ros2_amd import synthetic as S
 from trajectory_generator_ros2_amd.solver import Solver
 
 s = Solver(0)
-res = {"stepwise": bool(os.environ.get("TGMS_REFINE_STEPWISE"))}
-for name, (so, W, T) in {"uniform_M10": S.uniform_batch(65536, 10), "ragged_2_16": S.ragged_batch(65536, 2, 16)}.items():
+res = {"stepwise": bool(os.environ.get("TGMS_REFINE_STEPWISE")), "lib": os.path.basename(os.environ.get("TGMS_LIB", "default"))}
+NB = int(os.environ.get("REF_B", "65536"))
+for name, (so, W, T) in {"uniform_M10": S.uniform_batch(NB, 10), "ragged_2_16": S.ragged_batch(NB, 2, 16)}.items():
     so = np.asarray(so, dtype=np.int32)
     d_so = torch.from_numpy(so).cuda()
     dW = torch.from_numpy(np.ascontiguousarray(W).reshape(-1, 3)).cuda()
