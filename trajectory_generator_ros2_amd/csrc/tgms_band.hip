@@ -33,8 +33,8 @@ namespace {
 constexpr int KL = 9;              // sub-diagonals (== super-diagonals) of the interleaved KKT
 constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
-constexpr int UW = 32;             // scratch row: U row (19) + 3 eliminated right-hand sides, padded
-                                   // to one lane per entry of the half (stores need no lane mask)
+constexpr int UW = WC + 3;         // scratch row: U row (19) + 3 eliminated right-hand sides (lanes
+                                   // 0..21 of the half store, the rest are masked off)
 constexpr int HL = 32;             // lanes per trajectory
 #ifdef TGMS_BAND_STAMPS  // diagnostic build: s_memtime at phase boundaries, lane 0 of blocks < 64, first pair
 constexpr int BST_BLOCKS = 64, BST_STEPS = 160, BST_PH = 8;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR]
     BSTAMP(k, 4);
     // U row k: lane column c -> offset c - k (the diagonal stored inverted: back
     // substitution multiplies), right-hand sides at WC..WC+2, lanes beyond into padding
-    U[k * UW + (hl < WC ? (hl >= Lk ? hl - Lk : hl - Lk + WC) : hl)] = (hl == Lk) ? rp : n0;
+    if (hl < UW) U[k * UW + (hl < WC ? (hl >= Lk ? hl - Lk : hl - Lk + WC) : hl)] = (hl == Lk) ? rp : n0;
     __builtin_amdgcn_wave_barrier();  // slot is rewritten by the next step
     // slide: logical row 0's register becomes row k+10
     if (hl == Lk) col += WC;
