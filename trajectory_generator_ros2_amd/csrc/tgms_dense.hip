@@ -17,12 +17,12 @@ namespace {
 // Register-resident Gauss-Jordan elimination with partial pivoting (round 2).
 //
 // The KKT (N = 14M+2, plus the 3 right-hand sides as columns N..N+2) is spread over
-// a 256-thread workgroup as a 16 x 16 thread grid: thread (tr, tc) owns rows
-// r = tr + 16 i and columns c = tc + 16 j, at most 9 x 10 doubles at M = 10, in
-// registers.  Two workgroups (trajectories) per CU.  Step k: the pivot of column k is
-// the largest |a| over the rows not yet pivoted (candidates found by the column's
-// owners at the end of step k-1, reduced over 4 lanes per wave and 4 waves through
-// LDS); the pivot row's entries right of k and the column's multipliers go through
+// a 256-thread workgroup as a 16 x 16 thread grid: thread (tr, tc) = (tid % 16, tid / 16)
+// owns rows r = tr + 16 i and columns c = tc + 16 j, at most 9 x 10 doubles at M = 10,
+// in registers.  Two workgroups (trajectories) per CU.  Step k: the pivot of column k
+// is the largest |a| over the rows not yet pivoted, found by the column's 16 owners (one
+// 16-lane row of one wave, reduced by DPP) at the end of step k-1, so the other three
+// waves skip that search; the pivot row's entries right of k and the column's multipliers go through
 // LDS; every thread updates its block (column blocks left of k skipped: they are
 // done).  Gauss-Jordan eliminates column k from EVERY other row, so after N steps the
 // solution is x_k = b'_{p_k} / a_{p_k k}: no back substitution, which in registers
@@ -99,14 +99,17 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     __shared__ double s_ed[18];
     __shared__ double s_u[CJ * GJ_C];     // pivot row (columns right of k, 0 elsewhere)
     __shared__ double s_l[RI * GJ_G];     // multipliers (0 for the pivot row)
-    __shared__ double s_cv[2][GJ_T / W64];  // per-wave pivot candidates: |a|, a, row (double-buffered)
-    __shared__ double s_cs[2][GJ_T / W64];
-    __shared__ int s_ci[2][GJ_T / W64];
+    __shared__ double s_cv[2];              // pivot of the next column: |a|, a, row (double-buffered)
+    __shared__ double s_cs[2];
+    __shared__ int s_ci[2];
     __shared__ double s_ipiv[N];
     __shared__ int s_bad;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tr = tid / GJ_C, tc = tid % GJ_C;
+    // column-major grid: a column group's 16 threads are one 16-lane row of one wave, so
+    // the per-column work of a step (pivot candidates, multipliers) runs in one wave and
+    // the other three skip it (exec-mask branch), and its reduction stays in the row (DPP)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int tr = tid % GJ_G, tc = tid / GJ_G;
     const int32_t bi = blockIdx.x;
     const int32_t b = ids ? ids[bi] : bi;
     const int64_t s0 = seg_offsets ? (int64_t)seg_offsets[b] : (int64_t)b * M;
@@ -161,9 +164,12 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
 #pragma unroll
     for (int i = 0; i < RI; ++i) pos[i] = N;
 
-    // pivot candidates of column c (owners: tc == c % 16), reduced over the wave's 4
-    // row groups and left in slot `buf`
+    // pivot of column c (its owners: tc == c % 16, one 16-lane row): the largest |a|
+    // over the rows not yet pivoted, ties to the lowest row, reduced within the row by
+    // DPP (quad swaps, then half-row and row mirrors: every lane ends with the row's
+    // result) and left in slot `buf`
     auto candidates = [&](int c, int buf) {
+        if (tc != c % GJ_C) return;
         double best = -1.0, sv = 0.0;
         int brow = N;
         const int jc = c / GJ_C;
@@ -180,20 +186,21 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
                 }
             }
         }
-#pragma unroll
-        for (int off = GJ_C; off < W64; off <<= 1) {
-            const double ov = __shfl_xor(best, off, W64);
-            const double osv = __shfl_xor(sv, off, W64);
-            const int orow = __shfl_xor(brow, off, W64);
+        auto merge = [&](double ov, double osv, int orow) {
             const bool take = (ov > best) || (ov == best && orow < brow);
             best = take ? ov : best;
             sv = take ? osv : sv;
             brow = take ? orow : brow;
-        }
-        if (lane == (c % GJ_C)) {
-            s_cv[buf][wave] = best;
-            s_cs[buf][wave] = sv;
-            s_ci[buf][wave] = brow;
+        };
+        static_assert(GJ_G == 16, "a column group is one DPP row");
+        merge(dpp_f64<0xB1>(best), dpp_f64<0xB1>(sv), __builtin_amdgcn_mov_dpp(brow, 0xB1, 0xF, 0xF, false));
+        merge(dpp_f64<0x4E>(best), dpp_f64<0x4E>(sv), __builtin_amdgcn_mov_dpp(brow, 0x4E, 0xF, 0xF, false));
+        merge(dpp_f64<0x141>(best), dpp_f64<0x141>(sv), __builtin_amdgcn_mov_dpp(brow, 0x141, 0xF, 0xF, false));
+        merge(dpp_f64<0x140>(best), dpp_f64<0x140>(sv), __builtin_amdgcn_mov_dpp(brow, 0x140, 0xF, 0xF, false));
+        if (tr == 0) {
+            s_cv[buf] = best;
+            s_cs[buf] = sv;
+            s_ci[buf] = brow;
         }
     };
     candidates(0, 0);
@@ -202,24 +209,14 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     bool singular = false;
     for (int k = 0; k < N; ++k) {
         const int buf = k & 1;
-        // ---- the pivot: the largest candidate, ties to the lowest row ----
-        double pv = s_cv[buf][0], ps = s_cs[buf][0];
-        int p = s_ci[buf][0];
-#pragma unroll
-        for (int q = 1; q < GJ_T / W64; ++q) {
-            const double v = s_cv[buf][q], sv = s_cs[buf][q];
-            const int r = s_ci[buf][q];
-            const bool take = (v > pv) || (v == pv && r < p);
-            pv = take ? v : pv;
-            ps = take ? sv : ps;
-            p = take ? r : p;
-        }
-        p = __builtin_amdgcn_readfirstlane(p);
+        // ---- the pivot (found by column k's owners at the end of step k-1) ----
+        const double pv = s_cv[buf], ps = s_cs[buf];
+        const int p = __builtin_amdgcn_readfirstlane(s_ci[buf]);
         if (!(pv > 0.0)) {  // identical in every thread
             singular = true;
             break;
         }
-        const double ip = 1.0 / ps;
+        const double ip = fast_rcp(ps);  // within an ulp of 1 / ps
         if (tid == 0) s_ipiv[k] = ip;
         const int pg = p % GJ_G, pi = p / GJ_G;  // the pivot row's owners and their local row
         const int jk = k / GJ_C, kg = k % GJ_C;  // column k's owners and their local column
