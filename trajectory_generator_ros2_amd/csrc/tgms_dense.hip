@@ -97,10 +97,12 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     __shared__ double s_pw[M][8];
     __shared__ double s_w[(M + 1) * 3];
     __shared__ double s_ed[18];
-    __shared__ double s_u[CJ * GJ_C];     // pivot row (columns right of k, 0 elsewhere)
-    __shared__ double s_l[RI * GJ_G];     // multipliers (0 for the pivot row)
-    __shared__ double s_cv[2];              // pivot of the next column: |a|, a, row (double-buffered)
-    __shared__ double s_cs[2];
+    // pivot row and multipliers, one padded run per owner thread so the update reads
+    // them 16 B at a time: s_u[tc * US + j] = column tc + 16 j, s_l[tr * LS + i] = row tr + 16 i
+    constexpr int US = (CJ + 1) & ~1, LS = (RI + 1) & ~1;
+    __shared__ alignas(16) double s_u[GJ_C * US];  // pivot row (columns <= k stale: never read again)
+    __shared__ alignas(16) double s_l[GJ_G * LS];  // multipliers (0 for the pivot row)
+    __shared__ double s_cs[2];              // pivot of the next column: a, row (double-buffered)
     __shared__ int s_ci[2];
     __shared__ double s_ipiv[N];
     __shared__ int s_bad;
@@ -170,7 +172,10 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     // result) and left in slot `buf`
     auto candidates = [&](int c, int buf) {
         if (tc != c % GJ_C) return;
-        double best = -1.0, sv = 0.0;
+        // only the signed candidate travels; magnitudes are compared through abs
+        // modifiers.  No active row with a nonzero entry leaves brow = N and sv = 0: the
+        // pivot magnitude 0 then flags the matrix singular, as the first zero would.
+        double sv = 0.0;
         int brow = N;
         const int jc = c / GJ_C;
 #pragma unroll
@@ -178,27 +183,23 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
             if (j == jc) {
 #pragma unroll
                 for (int i = 0; i < RI; ++i) {
-                    const double v = fabs(a[i][j]);
-                    const bool take = ((act >> i) & 1u) && v > best;
-                    best = take ? v : best;
+                    const bool take = ((act >> i) & 1u) && fabs(a[i][j]) > fabs(sv);
                     sv = take ? a[i][j] : sv;
                     brow = take ? tr + GJ_G * i : brow;
                 }
             }
         }
-        auto merge = [&](double ov, double osv, int orow) {
-            const bool take = (ov > best) || (ov == best && orow < brow);
-            best = take ? ov : best;
+        auto merge = [&](double osv, int orow) {
+            const bool take = (fabs(osv) > fabs(sv)) || (fabs(osv) == fabs(sv) && orow < brow);
             sv = take ? osv : sv;
             brow = take ? orow : brow;
         };
         static_assert(GJ_G == 16, "a column group is one DPP row");
-        merge(dpp_f64<0xB1>(best), dpp_f64<0xB1>(sv), __builtin_amdgcn_mov_dpp(brow, 0xB1, 0xF, 0xF, false));
-        merge(dpp_f64<0x4E>(best), dpp_f64<0x4E>(sv), __builtin_amdgcn_mov_dpp(brow, 0x4E, 0xF, 0xF, false));
-        merge(dpp_f64<0x141>(best), dpp_f64<0x141>(sv), __builtin_amdgcn_mov_dpp(brow, 0x141, 0xF, 0xF, false));
-        merge(dpp_f64<0x140>(best), dpp_f64<0x140>(sv), __builtin_amdgcn_mov_dpp(brow, 0x140, 0xF, 0xF, false));
+        merge(dpp_f64<0xB1>(sv), __builtin_amdgcn_mov_dpp(brow, 0xB1, 0xF, 0xF, false));
+        merge(dpp_f64<0x4E>(sv), __builtin_amdgcn_mov_dpp(brow, 0x4E, 0xF, 0xF, false));
+        merge(dpp_f64<0x141>(sv), __builtin_amdgcn_mov_dpp(brow, 0x141, 0xF, 0xF, false));
+        merge(dpp_f64<0x140>(sv), __builtin_amdgcn_mov_dpp(brow, 0x140, 0xF, 0xF, false));
         if (tr == 0) {
-            s_cv[buf] = best;
             s_cs[buf] = sv;
             s_ci[buf] = brow;
         }
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     for (int k = 0; k < N; ++k) {
         const int buf = k & 1;
         // ---- the pivot (found by column k's owners at the end of step k-1) ----
-        const double pv = s_cv[buf], ps = s_cs[buf];
+        const double ps = s_cs[buf], pv = fabs(ps);
         const int p = __builtin_amdgcn_readfirstlane(s_ci[buf]);
         if (!(pv > 0.0)) {  // identical in every thread
             singular = true;
@@ -220,16 +221,16 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
         if (tid == 0) s_ipiv[k] = ip;
         const int pg = p % GJ_G, pi = p / GJ_G;  // the pivot row's owners and their local row
         const int jk = k / GJ_C, kg = k % GJ_C;  // column k's owners and their local column
-        // the pivot row right of k -> s_u (its owners: tr == pg)
+        // the pivot row -> s_u (its owners: tr == pg).  Only its columns right of k matter:
+        // the update then also changes columns <= k of block k / 16, which no later step
+        // and no output reads (candidates look right of k, the solution at the
+        // right-hand-side columns), so the row goes over whole.
         if (tr == pg) {
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
                 if (i == pi) {
 #pragma unroll
-                    for (int j = 0; j < CJ; ++j) {
-                        const int c = tc + GJ_C * j;
-                        s_u[c] = c > k ? a[i][j] : 0.0;
-                    }
+                    for (int j = 0; j < CJ; ++j) s_u[tc * US + j] = a[i][j];
                     pos[i] = k;
                 }
             }
@@ -243,22 +244,33 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
 #pragma unroll
                     for (int i = 0; i < RI; ++i) {
                         const int r = tr + GJ_G * i;
-                        s_l[r] = (r == p) ? 0.0 : a[i][j] * ip;
+                        s_l[tr * LS + i] = (r == p) ? 0.0 : a[i][j] * ip;
                     }
                 }
             }
         }
         __syncthreads();
         // ---- update: a -= l u over the thread's block (column blocks left of k are done) ----
-        double l[RI];
+        double l[LS], u[US];
 #pragma unroll
-        for (int i = 0; i < RI; ++i) l[i] = s_l[tr + GJ_G * i];
+        for (int q = 0; q < LS / 2; ++q) {
+            const double2 v = reinterpret_cast<const double2*>(s_l + tr * LS)[q];
+            l[2 * q] = v.x;
+            l[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int q = 0; q < US / 2; ++q) {
+            if (GJ_C * (2 * q + 1) + GJ_C - 1 > k) {  // uniform: a pair with a live column block
+                const double2 v = reinterpret_cast<const double2*>(s_u + tc * US)[q];
+                u[2 * q] = v.x;
+                u[2 * q + 1] = v.y;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < CJ; ++j) {
             if (GJ_C * j + GJ_C - 1 > k) {  // uniform
-                const double u = s_u[tc + GJ_C * j];
 #pragma unroll
-                for (int i = 0; i < RI; ++i) a[i][j] = __builtin_fma(-l[i], u, a[i][j]);
+                for (int i = 0; i < RI; ++i) a[i][j] = __builtin_fma(-l[i], u[j], a[i][j]);
             }
         }
         if (k + 1 < N) candidates(k + 1, buf ^ 1);
