@@ -11,17 +11,16 @@
 // that dense GEPP, not a band routine).  Flops: ~2 N kl (kl+ku) ~ 50 kflop at M = 10
 // against 2/3 N^3 = 1.9 MFLOP for the unordered dense LU (tgms_dense.hip).
 //
-// Mapping (gfx950): lanes 0..31 of a wavefront solve one trajectory, lanes 32..63 the
-// next.  Within a half, lane l < 19 owns the window column c = l (mod 19), lanes 19..21
-// the three right-hand sides (x, y, z share the matrix), so the active window (rows
-// k..k+9 x columns k..k+18) lives in 10 registers per lane and the elimination of column
-// k is 9 FMAs per lane.  The pivot column's lane picks the pivot, forms the 9
-// multipliers and hands them to its half through one LDS slot (in-order within the
-// wave: no barrier).  The entering row k+10 is assembled on the fly from the segment
-// powers T_i^e and the 2Q blocks staged in LDS (a1/a2 never exist as a matrix).
-// Each finished U row (19 entries + 3 eliminated right-hand sides, 176 B) goes to a
-// per-wave scratch slab; back substitution streams the slab in reverse with loads
-// issued 16 steps ahead, one lane per pending row, x_k broadcast through LDS.
+// Mapping (gfx950): a 16-lane DPP row per trajectory, four per wavefront, four
+// wavefronts per workgroup (sharing the entry table).  Forward elimination keeps one
+// window row per lane (row_step below): DPP pivot search, LDS broadcast of the pivot row,
+// 21 FMAs per lane and step, the entering row k+10 assembled column-parallel from the
+// segment powers T_i^e and the 2Q blocks staged in LDS (a1/a2 never exist as a matrix).
+// Each finished U row (1/pivot, 18 super-diagonal entries, 3 eliminated right-hand
+// sides: 176 B) goes to a per-trajectory slab; back substitution (back_step) streams
+// the slab in reverse, a 16-B piece of a row per lane, as a DPP dot product.
+// Round 2's first mapping (a half-wavefront per trajectory, lane = window column) took
+// 2.50 ms per 65,536 at M = 10; this one 1.69 ms.
 #include <algorithm>
 
 #include "tgms_device.h"
@@ -33,24 +32,7 @@ namespace {
 constexpr int KL = 9;              // sub-diagonals (== super-diagonals) of the interleaved KKT
 constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
-constexpr int UW = WC + 3;         // scratch row: U row (19) + 3 eliminated right-hand sides (lanes
-                                   // 0..21 of the half store, the rest are masked off)
-constexpr int HL = 32;             // lanes per trajectory
-#ifdef TGMS_BAND_STAMPS  // diagnostic build: s_memtime at phase boundaries, lane 0 of blocks < 64, first pair
-constexpr int BST_BLOCKS = 64, BST_STEPS = 160, BST_PH = 8;
-__device__ unsigned long long g_bstamps[BST_BLOCKS * BST_STEPS * BST_PH];
-#define BSTAMP(k, i)                                                                                    \
-    do {                                                                                                \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                     \
-        if (blockIdx.x < BST_BLOCKS && threadIdx.x == 0 && (k) < BST_STEPS && first_pair)              \
-            g_bstamps[(blockIdx.x * BST_STEPS + (k)) * BST_PH + (i)] = __builtin_amdgcn_s_memtime();     \
-    } while (0)
-#else
-#define BSTAMP(k, i) \
-    do {             \
-    } while (0)
-#endif
-constexpr int PFB = 16;            // back-substitution prefetch depth (steps)
+constexpr int UW = WC + 3;         // slab row: U row (19) + 3 eliminated right-hand sides
 
 // Position q of the interleaved order.  kind: 0 start row (idx = derivative k),
 // 1 coefficient (seg, idx = power j), 2 interior-knot row after segment seg
@@ -168,11 +150,6 @@ __device__ __forceinline__ double row_entry(int hl, int r, int c, const int* des
     return (hl < WC) ? (inb ? m : 0.0) : ((hl < WC + 3) ? rhs : 0.0);
 }
 
-// U-slab load that misses L1 (an agent-scope relaxed atomic load: sc1)
-__device__ __forceinline__ double ld_u(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // 1/x: hardware reciprocal + two Newton steps (within an ulp; the pivots only scale)
 __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
@@ -180,255 +157,373 @@ __device__ __forceinline__ double recip(double x) {
     return fma(r, fma(-x, r, 1.0), r);
 }
 
-// One elimination step k; logical window row i lives in a[(R0 + i) % WR].
-template <int M, bool HAS_ED, int R0>
-__device__ __forceinline__ void elim_step(int k, int Lk, int hl, double (&a)[WR], int& col, bool& sing,
-                                          double* slot, double* U, const int* desc, const double* val,
-                                          const double* w, const double* ed, bool first_pair) {
-#define A_(i) a[(R0 + (i)) % WR]
-    BSTAMP(k, 0);
-    // pivot search in every lane's own column; the pivot column's lane Lk decides
-    double bv = A_(0);
-    int p = 0;
-#pragma unroll
-    for (int i = 1; i < WR; ++i) {
-        const bool g = fabs(A_(i)) > fabs(bv);
-        bv = g ? A_(i) : bv;
-        p = g ? i : p;
-    }
-    BSTAMP(k, 1);
-    // the two halves' pivot rows (lanes Lk and Lk + 32) through the scalar unit
-    const int p0 = __builtin_amdgcn_readlane(p, Lk), p1 = __builtin_amdgcn_readlane(p, Lk + HL);
-    // row interchange 0 <-> P in every column (selects: a branch per pivot row makes the
-    // register allocator copy the whole window at every join)
-    const int P = (hl == threadIdx.x) ? p0 : p1;
-    const double v0 = A_(0);
-    double n0 = v0;
-#pragma unroll
-    for (int i = 1; i < WR; ++i) {
-        const bool s = (P == i);
-        n0 = s ? A_(i) : n0;
-        A_(i) = s ? v0 : A_(i);
-    }
-    const double best = fabs(bv);
-    BSTAMP(k, 2);
-    // multipliers of the pivot column, handed to the half through LDS (in order within
-    // the wavefront, so no barrier)
-    // The pivot column leaves the window (its lane takes column k+19, zero in rows
-    // k+1..k+9): its rows are cleared here and its update below multiplies by 0.
-    double nu = n0;
-    const double rp = recip(n0);
-    if (hl == Lk) {
-        sing = sing || !(best > 0.0);
-#pragma unroll
-        for (int i = 1; i < WR; ++i) {
-            slot[i] = A_(i) * rp;
-            A_(i) = 0.0;
-        }
-        nu = 0.0;
-    }
-    BSTAMP(k, 3);
-    __builtin_amdgcn_wave_barrier();
-    double l[WR];
-#pragma unroll
-    for (int i = 1; i < WR; ++i) l[i] = slot[i];
-    // rank-1 update
-#pragma unroll
-    for (int i = 1; i < WR; ++i) A_(i) = fma(-l[i], nu, A_(i));
-    BSTAMP(k, 4);
-    // U row k: lane column c -> offset c - k (the diagonal stored inverted: back
-    // substitution multiplies), right-hand sides at WC..WC+2, lanes beyond into padding
-    if (hl < UW) U[k * UW + (hl < WC ? (hl >= Lk ? hl - Lk : hl - Lk + WC) : hl)] = (hl == Lk) ? rp : n0;
-    __builtin_amdgcn_wave_barrier();  // slot is rewritten by the next step
-    // slide: logical row 0's register becomes row k+10
-    if (hl == Lk) col += WC;
-    A_(0) = row_entry<M, HAS_ED>(hl, k + WR, col, desc, val, w, ed);
-    BSTAMP(k, 6);
-#undef A_
+// ---------------------------------------------------------------------------
+// Row-lane mapping: a 16-lane DPP row per trajectory, four trajectories per wavefront.
+// Lane j < WR holds one window row: its entries at columns k..k+18 in registers
+// u[c mod 19] (static register names under a 19-step unroll) and its 3 right-hand
+// sides.  Rows never move between lanes: the pivot search is a DPP max over the row's
+// lanes (ties to the lowest position in the permuted order, as LAPACK and the oracle),
+// the interchange is a swap of two position labels, and the pivot row reaches the other
+// lanes through one LDS broadcast.  The pivot lane leaves with its row (it becomes U row
+// k in the slab) and takes the entering row k+10, which the group assembles
+// column-parallel (two entries per lane) and hands over through LDS.  A step issues
+// ~160 VALU + ~100 SALU instructions per wavefront for four trajectories (the
+// column-lane mapping: ~105 VALU + ~40 SALU for two).
+constexpr int QG = 16;                  // lanes per trajectory (one DPP row)
+constexpr int QT = W64 / QG;            // trajectories per wavefront
+constexpr int QW = 4;                   // wavefronts per workgroup (share the entry table)
+constexpr int QS = UW + 2;              // LDS row stride of the pivot / entering rows (16-B aligned)
+#ifndef TGMS_BAND_WAVES_PER_EU
+#define TGMS_BAND_WAVES_PER_EU 2           // register budget: 256 VGPRs, no spills in the step loops
+#endif
+
+using gdouble = __attribute__((address_space(1))) double;  // global: keeps slab accesses off the flat path
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
 }
 
-constexpr int TGMS_BAND_LB = 1;  // minimum wavefronts per SIMD the register allocation must allow
+// Column held by register t at step k (R = k mod WC): the c = t (mod WC) in [k+1, k+WC]
+// once column k has left (the entering row's columns).
+template <int R>
+__device__ __forceinline__ int enter_col(int k, int t) {
+    int d = t - (R + 1) % WC;
+    d += (d < 0) ? WC : 0;
+    return k + 1 + d;
+}
+
+// Lane-dependent values re-derived inside every unrolled step: an opaque copy keeps
+// LICM from hoisting 19 steps' worth of per-lane index arithmetic (and its registers)
+// out of the step loops.
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ gdouble* opaque(gdouble* p) {
+    asm volatile("" : "+v"(p));
+    return p;
+}
+
+// Entering row k+WR, column-parallel and branch-free: lane j assembles register slot j,
+// lanes 0..2 also slots 16..18 and lanes 3..5 the right-hand sides (slots 19..21).  The
+// row's block, offset and right-hand-side source are wave-uniform (scalar unit).  Same
+// entries as row_entry.
+template <int M, bool HAS_ED, int R>
+__device__ __forceinline__ void enter_row(int k, int j, const int* desc, const double* val, const double* w,
+                                          const double* ed, double* E) {
+    constexpr int N = 14 * M + 2;
+    const int r = k + WR;
+    const bool live_r = r < N;
+    const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
+    const int o = live_r ? r - (4 + 14 * i) : 0;
+    int wr = -1, eb = -1;
+    if (o < 0) {
+        if (o == -4) wr = 0;
+        else eb = (o + 3) * 3;
+    } else if (o >= 8) {
+        const int t = o - 8;
+        if (i == M - 1) {
+            if (t == 0) wr = M;
+            else eb = 9 + (t - 1) * 3;
+        } else if (t <= 1) {
+            wr = i + 1;
+        }
+    }
+    const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
+    const int* drow = desc + (vv * NOFF + o + 4) * WC + KL;
+    const double* vrow = val + i * VAL;
+    auto entry = [&](int c) {
+        const int d = c - r;
+        const bool inb = live_r && c < N && d >= -KL && d <= KL;
+        const int de = drow[min(max(d, -KL), KL)];
+        const double m = (double)(de >> 5) * vrow[de & 31];
+        return inb ? m : 0.0;
+    };
+    const double e0 = entry(enter_col<R>(k, j));
+    const double e1 = entry(enter_col<R>(k, min(j + QG, WC - 1)));
+    const int ax = min(max(j - 3, 0), 2);
+    const double rw = w[max(wr, 0) * 3 + ax];
+    const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
+    const double rhs = (live_r && wr >= 0) ? rw : ((HAS_ED && live_r && eb >= 0) ? re : 0.0);
+    E[j] = e0;
+    if (j < 6) E[QG + j] = (j < 3) ? e1 : rhs;
+}
+
+template <int M, bool HAS_ED, int R>
+__device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double (&rh)[3], int& pos, bool& sing,
+                                         double* P, double* E, gdouble* U, const int* desc, const double* val,
+                                         const double* w, const double* ed) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int j = opaque(j0);
+    enter_row<M, HAS_ED, R>(k, j, desc, val, w, ed, E);
+    // pivot search in column k (register R) over the window lanes: DPP max of |a|, then
+    // the lowest position among the maxima
+    const double cv = u[R];
+    const bool win = j < WR;
+    double m = win ? fabs(cv) : -1.0;
+    m = fmax(m, dpp_f64<0xB1>(m));   // quad_perm [1,0,3,2]
+    m = fmax(m, dpp_f64<0x4E>(m));   // quad_perm [2,3,0,1]
+    m = fmax(m, dpp_f64<0x141>(m));  // row_half_mirror
+    m = fmax(m, dpp_f64<0x140>(m));  // row_mirror
+    const bool eq = win && fabs(cv) == m;
+    int cp = eq ? pos : 0x7fffffff;
+    cp = min(cp, dpp_i32<0xB1>(cp));
+    cp = min(cp, dpp_i32<0x4E>(cp));
+    cp = min(cp, dpp_i32<0x141>(cp));
+    cp = min(cp, dpp_i32<0x140>(cp));
+    const bool piv = eq && pos == cp;
+    sing = sing || !(m > 0.0);
+    // the pivot lane hands its row to the group through LDS ([1/pivot, columns
+    // k+1..k+18, rhs]: U row k), one 64-bit write per entry (no register shuffles)
+    if (piv) {
+        P[0] = recip(cv);
+#pragma unroll
+        for (int d = 1; d < WC; ++d) P[d] = u[(R + d) % WC];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) P[WC + a] = rh[a];
+    }
+    __builtin_amdgcn_wave_barrier();
+    double p[UW];
+    {
+        const double2* Pd = reinterpret_cast<const double2*>(P);
+#pragma unroll
+        for (int q = 0; q < UW / 2; ++q) {
+            const double2 v = Pd[q];
+            p[2 * q] = v.x;
+            p[2 * q + 1] = v.y;
+        }
+        // U row k to the slab: lane j < 11 copies 16 B of it
+        if (j < UW / 2) {
+            const double2 v = Pd[j];
+            gdouble* Uk = U + (size_t)k * UW + 2 * j;
+            Uk[0] = v.x;
+            Uk[1] = v.y;
+        }
+    }
+    // rank-1 update of the other window rows; column k leaves (register R becomes
+    // column k+19, zero outside the entering row)
+    const double l = (win && !piv) ? cv * p[0] : 0.0;
+#pragma unroll
+    for (int d = 1; d < WC; ++d) u[(R + d) % WC] = fma(-l, p[d], u[(R + d) % WC]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rh[a] = fma(-l, p[WC + a], rh[a]);
+    u[R] = 0.0;
+    if (pos == k) pos = cp;  // interchange: the row at position k takes the pivot's position
+    if (piv) {               // the pivot lane takes row k+WR
+#pragma unroll
+        for (int t = 0; t < WC; ++t) u[t] = E[t];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) rh[a] = E[WC + a];
+        pos = k + WR;
+    }
+    __builtin_amdgcn_wave_barrier();  // P and E are rewritten by the next step
+}
+
+// Back substitution of one trajectory by its 16-lane row, row oriented:
+//   x_k = (b'_k - sum_{d=1..18} U[k][k+d] x_{k+d}) / U[k][k].
+// Lane j < 11 holds 16 B of U row k, (U[k][2j], U[k][2j+1]), and the matching window
+// values (x_{k+2j}, x_{k+2j+1}) for 3 axes; the dot product is a DPP butterfly over the
+// row.  The eliminated right-hand side rides in the same sum: lanes 9 and 10 hold the
+// constants -e_a against U[k][19..21], and lane 0's x_k slot is 0 against 1/U[k][k].
+// Lane 0 finalizes x_k = -sum * (1/U[k][k]) and the window slides one position (DPP
+// row shift), so x_k never leaves the registers.  Rows come through a 19-deep ring of
+// 16-B buffer loads issued one lap ahead (every ring slot its own register, every lane
+// loading: no load result is read before its lap is over).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int BCPOL_SC1 = 16;  // agent-scope (L1-bypassing) load: the slab was written by this wave
+
+template <bool BOUND_ZERO>
+__device__ __forceinline__ double dpp_shr1_f64(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x111, 0xF, 0xF, BOUND_ZERO);  // row_shr:1
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xF, 0xF, BOUND_ZERO);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double2 ld_row16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, BCPOL_SC1));
+}
+
+// byte offset of lane j's 16 B of row kk in the wave's slabs (out of range: 0 returned)
+__device__ __forceinline__ uint32_t row_off(int g, int j, int kk, int N) {
+    return (kk >= 0 && j < UW / 2) ? (uint32_t)(((g * N + kk) * UW + 2 * j) * 8) : 0xFFFFFFF0u;
+}
+
+template <int M, int S>
+__device__ __forceinline__ void back_step(int k, int j0, int g, __amdgpu_buffer_rsrc_t rs, double2 (&ur)[WC],
+                                          double (&xa)[3], double (&xb)[3], double* out, bool live, bool emit,
+                                          double& fin) {
+    constexpr int N = 14 * M + 2;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int j = opaque(j0);
+    const double2 uk = ur[S];
+    double sm[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) sm[a] = fma(uk.y, xb[a], uk.x * xa[a]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        sm[a] += dpp_f64<0xB1>(sm[a]);   // quad_perm [1,0,3,2]
+        sm[a] += dpp_f64<0x4E>(sm[a]);   // quad_perm [2,3,0,1]
+        sm[a] += dpp_f64<0x141>(sm[a]);  // row_half_mirror
+        sm[a] += dpp_f64<0x140>(sm[a]);  // row_mirror
+    }
+    // lane 0: uk.x = 1 / U[k][k]
+    double x[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) x[a] = -sm[a] * uk.x;
+    if (j == 0 && k >= 0) {
+        fin += (x[0] + x[1] + x[2]) * 0.0;
+        const Pos pk = decode<M>(k);
+        if (pk.kind == 1 && live) {
+            double* o = out + pk.seg * 24 + pk.idx;
+            o[0] = emit ? x[0] : 0.0;
+            o[8] = emit ? x[1] : 0.0;
+            o[16] = emit ? x[2] : 0.0;
+        }
+    }
+    // slide the window: (x_{k+2j}, x_{k+2j+1}) -> (x_{k-1+2j}, x_{k+2j}); lanes 9 and 10
+    // keep the right-hand-side constants
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double cur = (j == 0) ? x[a] : xa[a];
+        const double nxa = dpp_shr1_f64<true>(xb[a]);
+        xb[a] = (j == 9) ? (a == 0 ? -1.0 : 0.0) : ((j == 10) ? (a == 2 ? -1.0 : 0.0) : cur);
+        xa[a] = (j == 10) ? (a == 1 ? -1.0 : 0.0) : nxa;
+    }
+    // refill the ring slot for step k-19 (same slot)
+    ur[S] = ld_row16(rs, row_off(g, j, k - WC, N));
+}
 
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(W64, TGMS_BAND_LB) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
-                                                  const int32_t* __restrict__ seg_offsets,
-                                                  const double* __restrict__ W, const double* __restrict__ T,
-                                                  const double* __restrict__ ED, double* __restrict__ C,
-                                                  int32_t* __restrict__ status, double* __restrict__ scratch) {
+__global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_BAND_WAVES_PER_EU))) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
+                                                       const int32_t* __restrict__ seg_offsets,
+                                                       const double* __restrict__ W, const double* __restrict__ T,
+                                                       const double* __restrict__ ED, double* __restrict__ C,
+                                                       int32_t* __restrict__ status, double* __restrict__ scratch) {
     constexpr int N = 14 * M + 2;
-    __shared__ int s_desc[NDESC];           // entry pattern of the interleaved KKT
-    __shared__ double s_val[2][M * VAL];    // V_i = [1, T_i^0..T_i^7, 2Q_i] per segment
-    __shared__ double s_w[2][(M + 1) * 3];  // waypoints
-    __shared__ double s_ed[2][18];          // end derivatives (HAS_ED)
-    __shared__ double s_slot[2][WR];        // pivot index + multipliers of the current step
-    __shared__ double s_x[2][4];            // back substitution: x_k broadcast
+    __shared__ int s_desc[NDESC];                            // entry pattern of the interleaved KKT
+    __shared__ double s_val[QW][QT][M * VAL];                // V_i = [1, T_i^0..T_i^7, 2Q_i] per segment
+    __shared__ double s_w[QW][QT][(M + 1) * 3];              // waypoints
+    __shared__ double s_ed[QW][QT][HAS_ED ? 18 : 1];         // end derivatives
+    __shared__ alignas(16) double s_piv[QW][QT][QS];         // pivot row of the current step
+    __shared__ alignas(16) double s_ent[QW][QT][QS];         // entering row of the current step
+    __shared__ double s_x[QW][QT][4];                        // back substitution: x_k broadcast
 
-    const int lane = threadIdx.x, h = lane >> 5, hl = lane & (HL - 1);
-    double* U = scratch + ((size_t)blockIdx.x * 2 + h) * (size_t)N * UW;
-    double* val = s_val[h];
-    for (int q = lane; q < NDESC; q += W64) {
+    const int wv = threadIdx.x / W64, lane = threadIdx.x % W64, g = lane / QG;
+    for (int q = threadIdx.x; q < NDESC; q += QW * W64) {
         const int vv = q / (NOFF * WC), rem = q - vv * NOFF * WC, o = rem / WC - 4, d = rem % WC - KL;
         s_desc[q] = desc_entry(vv, o, d);
     }
-    double* w = s_w[h];
-    double* ed = s_ed[h];
-    double* slot = s_slot[h];
-    const int npairs = (n_traj + 1) >> 1;
+    __syncthreads();
+    const int wave_id = blockIdx.x * QW + wv;
+    gdouble* const U0 = (gdouble*)scratch + ((size_t)wave_id * QT + g) * (size_t)N * UW;
+    double* val = s_val[wv][g];
+    double* w = s_w[wv][g];
+    double* ed = s_ed[wv][g];
+    double* P = s_piv[wv][g];
+    double* E = s_ent[wv][g];
+    double* xs = s_x[wv][g];
+    const int nquads = (n_traj + QT - 1) / QT;
 
-    for (int pr = blockIdx.x; pr < npairs; pr += gridDim.x) {
-        const bool first_pair = pr == (int)blockIdx.x;
-        (void)first_pair;
-        const int bi = 2 * pr + h;
+    for (int qd = wave_id; qd < nquads; qd += gridDim.x * QW) {
+        // per-quad opaque copies: the slab addresses must not be hoisted out of this loop
+        gdouble* const U = opaque(U0);
+        const int j = opaque(lane % QG);
+        const int bi = QT * qd + g;
         const bool live = bi < n_traj;
-        const int32_t b = ids ? ids[live ? bi : 2 * pr] : (live ? bi : 2 * pr);
+        const int32_t b = ids ? ids[live ? bi : QT * qd] : (live ? bi : QT * qd);
         const int64_t s0 = seg_offsets ? (int64_t)seg_offsets[b] : (int64_t)b * M;
         const double* gw = W + (s0 + b) * 3;
         const double* gt = T + s0;
 
         // ---- stage inputs, validate (T > 0 finite; W, ED finite)
         bool ok = true;
-        for (int q = hl; q < (M + 1) * 3; q += HL) {
+        for (int q = j; q < (M + 1) * 3; q += QG) {
             const double v = gw[q];
             w[q] = v;
             ok = ok && (v * 0.0 == 0.0);
         }
-        if (HAS_ED && hl < 18) {
-            const double v = ED[(int64_t)b * 18 + hl];
-            ed[hl] = v;
-            ok = ok && (v * 0.0 == 0.0);
+        if (HAS_ED) {
+            for (int q = j; q < 18; q += QG) {
+                const double v = ED[(int64_t)b * 18 + q];
+                ed[q] = v;
+                ok = ok && (v * 0.0 == 0.0);
+            }
         }
-        if (hl < M) {
-            const double t = gt[hl];
+        for (int i = j; i < M; i += QG) {
+            const double t = gt[i];
             ok = ok && finite_pos(t);
             double p = 1.0;
-            val[hl * VAL] = 1.0;
-            val[hl * VAL + 1] = 1.0;
+            val[i * VAL] = 1.0;
+            val[i * VAL + 1] = 1.0;
 #pragma unroll
             for (int e = 1; e < 8; ++e) {
                 p *= t;
-                val[hl * VAL + 1 + e] = p;
+                val[i * VAL + 1 + e] = p;
             }
         }
         const unsigned long long badm = __ballot(!ok);
-        const bool valid = ((h ? (badm >> 32) : badm) & 0xffffffffull) == 0;
+        const bool valid = ((badm >> (QG * g)) & 0xffffull) == 0;
         __builtin_amdgcn_wave_barrier();
-        for (int q = hl; q < M * 16; q += HL) {
-            const int i = q >> 4, j = 4 + ((q >> 2) & 3), kk = 4 + (q & 3), ex = j + kk - 7;
-            val[i * VAL + 9 + (q & 15)] = 2.0 * (dfac(j, 4) * dfac(kk, 4) * val[i * VAL + 1 + ex] / (double)ex);
+        for (int q = j; q < M * 16; q += QG) {
+            const int i = q >> 4, jj = 4 + ((q >> 2) & 3), kk = 4 + (q & 3), ex = jj + kk - 7;
+            val[i * VAL + 9 + (q & 15)] = 2.0 * (dfac(jj, 4) * dfac(kk, 4) * val[i * VAL + 1 + ex] / (double)ex);
         }
         __builtin_amdgcn_wave_barrier();
 
-        // ---- forward elimination (a3): window rows 0..9, columns hl
-        int col = hl;
-        double a[WR];
+        // ---- forward elimination (a3): lane j < WR holds window row j
+        double u[WC], rh[3];
+        int pos = (j < WR) ? j : -1;  // position in the permuted order (-1: not a window lane)
 #pragma unroll
-        for (int i = 0; i < WR; ++i) a[i] = row_entry<M, HAS_ED>(hl, i, col, s_desc, val, w, ed);
+        for (int t = 0; t < WC; ++t) u[t] = (j < WR) ? row_entry<M, HAS_ED>(t, j, t, s_desc, val, w, ed) : 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) rh[a] = (j < WR) ? row_entry<M, HAS_ED>(WC + a, j, 0, s_desc, val, w, ed) : 0.0;
         bool sing = false;
-        int Lk = 0;
-        for (int k0 = 0; k0 < N; k0 += WR) {
-#define STEP(R)                                                                                         \
-    if (k0 + R < N) {                                                                                   \
-        elim_step<M, HAS_ED, R>(k0 + R, Lk, hl, a, col, sing, slot, U, s_desc, val, w, ed, first_pair);              \
-        Lk = (Lk == WC - 1) ? 0 : Lk + 1;                                                               \
-    }
+        for (int k0 = 0; k0 < N; k0 += WC) {
+#define STEP(R) \
+    if (k0 + R < N) row_step<M, HAS_ED, R>(k0 + R, j, u, rh, pos, sing, P, E, U, s_desc, val, w, ed);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
+            STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
         }
         const unsigned long long singm = __ballot(sing);
-        const bool singular = ((h ? (singm >> 32) : singm) & 0xffffffffull) != 0;
+        const bool singular = ((singm >> (QG * g)) & 0xffffull) != 0;
         const bool emit = live && valid && !singular;
 
-        // ---- back substitution, column oriented: lane hl < WC holds y for the pending
-        // row r = hl (mod WC) in [k-18, k]; at step k that row needs U[r][k-r].
-        // The U rows this wave stored are read back by other lanes of the wave: wait for
-        // the stores to reach L2, and read them with L1-bypassing loads (ld_u: the slab is
-        // reused by the next pair, so L1 may hold the previous pair's lines).  An
-        // agent-scope fence here instead (buffer_wbl2: write back the XCD's L2) cost the
-        // whole kernel.
+        // ---- back substitution.  The U rows this wave stored are read back by other lanes
+        // of the wave: wait for the stores to reach L2 and read them with L1-bypassing loads
+        // (the slab is reused by the next quad, so L1 may hold the previous one's lines)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // Lane hl < WC holds y of its pending row r = hl (mod WC) in [k-18, k] and, loaded
-        // a full lap (19 steps) ahead, the eliminated right-hand side of its next row r-19.
-        // At step k it needs U[r][k-r]: those come through a PFB-deep ring of loads.
-        const int kN = N - 1;
-        int LkB = kN % WC;
-        double y0 = 0.0, y1 = 0.0, y2 = 0.0, yb0 = 0.0, yb1 = 0.0, yb2 = 0.0;
-        if (hl < WC) {
-            const int d = (LkB >= hl) ? LkB - hl : LkB - hl + WC;
-            const int r = kN - d;
-            if (r >= 0) {
-                const double* ur = U + (size_t)r * UW + WC;
-                y0 = ld_u(ur);
-                y1 = ld_u(ur + 1);
-                y2 = ld_u(ur + 2);
-            }
-            if (r - WC >= 0) {
-                const double* ur = U + (size_t)(r - WC) * UW + WC;
-                yb0 = ld_u(ur);
-                yb1 = ld_u(ur + 1);
-                yb2 = ld_u(ur + 2);
-            }
-        }
-        double ud[PFB];
-        auto issue = [&](int k, int slotk, int lk) {
-            const int d = (lk >= hl) ? lk - hl : lk - hl + WC;
-            ud[slotk] = (k >= 0 && hl < WC && k - d >= 0) ? ld_u(U + (size_t)(k - d) * UW + d) : 0.0;
-        };
-        int lkPF = LkB;
+        constexpr int kN = N - 1;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            scratch + (size_t)wave_id * QT * N * UW, (short)0, QT * N * UW * 8, 0x00020000);
+        double2 ur[WC];
 #pragma unroll
-        for (int s = 0; s < PFB; ++s) {
-            issue(kN - s, s, lkPF);
-            lkPF = (lkPF == 0) ? WC - 1 : lkPF - 1;
+        for (int S = 0; S < WC; ++S) ur[S] = ld_row16(rs, row_off(g, j, kN - S, N));
+        double xa[3], xb[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            xa[a] = (j == 10) ? (a == 1 ? -1.0 : 0.0) : 0.0;
+            xb[a] = (j == 9) ? (a == 0 ? -1.0 : 0.0) : ((j == 10) ? (a == 2 ? -1.0 : 0.0) : 0.0);
         }
-        double* xs = s_x[h];
         double* out = C + s0 * 24;
         double fin = 0.0;
-        for (int k0 = kN; k0 >= 0; k0 -= PFB) {
-#pragma unroll
-            for (int s = 0; s < PFB; ++s) {
-                const int k = k0 - s;
-                if (k >= 0) {
-                    const double u = ud[s];
-                    if (hl == LkB) {  // u = 1 / U[k][k]
-                        const double x0 = y0 * u, x1 = y1 * u, x2 = y2 * u;
-                        xs[0] = x0;
-                        xs[1] = x1;
-                        xs[2] = x2;
-                        fin += (x0 + x1 + x2) * 0.0;
-                        const Pos pk = decode<M>(k);
-                        if (pk.kind == 1 && live) {
-                            double* o = out + pk.seg * 24 + pk.idx;
-                            o[0] = emit ? x0 : 0.0;
-                            o[8] = emit ? x1 : 0.0;
-                            o[16] = emit ? x2 : 0.0;
-                        }
-                        // take row k-19 (its right-hand side arrived a lap ago), fetch the next
-                        y0 = yb0;
-                        y1 = yb1;
-                        y2 = yb2;
-                        if (k - 2 * WC >= 0) {
-                            const double* ur = U + (size_t)(k - 2 * WC) * UW + WC;
-                            yb0 = ld_u(ur);
-                            yb1 = ld_u(ur + 1);
-                            yb2 = ld_u(ur + 2);
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    const double x0 = xs[0], x1 = xs[1], x2 = xs[2];
-                    if (hl < WC && hl != LkB) {
-                        y0 = fma(-u, x0, y0);
-                        y1 = fma(-u, x1, y1);
-                        y2 = fma(-u, x2, y2);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    issue(k - PFB, s, lkPF);
-                    LkB = (LkB == 0) ? WC - 1 : LkB - 1;
-                    lkPF = (lkPF == 0) ? WC - 1 : lkPF - 1;
-                }
-            }
+#ifdef TGMS_BAND_NOBACK  // ablation build: forward elimination only
+        for (int k0 = kN; k0 >= 0 && false; k0 -= WC) {
+#else
+        for (int k0 = kN; k0 >= 0; k0 -= WC) {
+#endif
+#define BSTEP(S) back_step<M, S>(k0 - S, j, g, rs, ur, xa, xb, out, live, emit, fin);
+            BSTEP(0) BSTEP(1) BSTEP(2) BSTEP(3) BSTEP(4) BSTEP(5) BSTEP(6) BSTEP(7) BSTEP(8) BSTEP(9)
+            BSTEP(10) BSTEP(11) BSTEP(12) BSTEP(13) BSTEP(14) BSTEP(15) BSTEP(16) BSTEP(17) BSTEP(18)
+#undef BSTEP
         }
         const unsigned long long nf = __ballot(!(fin == 0.0));
-        const bool nonfinite = ((h ? (nf >> 32) : nf) & 0xffffffffull) != 0;
-        if (live && hl == 0 && status) {
+        const bool nonfinite = ((nf >> (QG * g)) & 0xffffull) != 0;
+        if (live && j == 0 && status) {
             int32_t st = TGMS_OK;
             if (!valid) st = TGMS_ERR_INVALID_ARG;
             else if (singular) st = TGMS_ERR_SINGULAR;
@@ -444,30 +539,35 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
                   const double* ED, double* C, int32_t* status, double* scratch, int32_t grid,
                   hipStream_t stream) {
     if (n_traj <= 0) return hipSuccess;
-    // persistent grid: only as many wavefronts as are resident at once (a second,
-    // partial round of wavefronts would double the tail)
+    // persistent grid of resident workgroups only (a second, partial round would double
+    // the tail); `grid` counts wavefronts, each with QT slabs
     static int occ[2] = {0, 0};
     int& nb = occ[ED ? 1 : 0];
     if (nb == 0) {
-        hipError_t e = ED ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, true>, W64, 0)
-                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, false>, W64, 0);
-        if (e != hipSuccess || nb <= 0) nb = BAND_WAVES_PER_CU;
+        hipError_t e = ED ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, true>, QW * W64, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_band_kkt<M, false>, QW * W64, 0);
+        if (e != hipSuccess || nb <= 0) nb = 1;
     }
-    const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, BAND_WAVES_PER_CU);
-    const int32_t g = std::min<int32_t>(std::min(grid, resident), (n_traj + 1) / 2);
+    constexpr int kMaxBlocksPerCU = BAND_WAVES_PER_CU / QW;
+    const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, kMaxBlocksPerCU);
+    const int32_t nquads = (n_traj + QT - 1) / QT;
+    const int32_t g = std::max<int32_t>(1, std::min<int32_t>(resident, (nquads + QW - 1) / QW));
     if (ED)
-        TGMS_LAUNCH((k_band_kkt<M, true>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
-                           status, scratch);
+        TGMS_LAUNCH((k_band_kkt<M, true>), dim3(g), dim3(QW * W64), 0, stream, n_traj, ids, so, W, T, ED, C,
+                    status, scratch);
     else
-        TGMS_LAUNCH((k_band_kkt<M, false>), dim3(g), dim3(W64), 0, stream, n_traj, ids, so, W, T, ED, C,
-                           status, scratch);
+        TGMS_LAUNCH((k_band_kkt<M, false>), dim3(g), dim3(QW * W64), 0, stream, n_traj, ids, so, W, T, ED, C,
+                    status, scratch);
     return hipSuccess;
 }
+
+constexpr int SLABS_PER_WAVE = QT;
+
 
 }  // namespace
 
 size_t band_scratch_bytes(int M, int32_t grid) {
-    return (size_t)grid * 2 * (size_t)(14 * M + 2) * UW * sizeof(double);
+    return (size_t)grid * SLABS_PER_WAVE * (size_t)(14 * M + 2) * UW * sizeof(double);
 }
 
 hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* ids, const int32_t* so, const double* W,
@@ -476,16 +576,14 @@ hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* ids, const int3
     switch (M) {
 #define X(m) \
     case m: return band_M<m>(n_traj, ids, so, W, T, ED, C, status, scratch, grid, stream);
+#ifdef TGMS_BAND_ONLY_M10  // development builds: one instantiation
+        X(10)
+#else
         X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+#endif
 #undef X
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace tgms
-
-#ifdef TGMS_BAND_STAMPS
-extern "C" int tgms_debug_band_stamps(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tgms::g_bstamps), sizeof(unsigned long long) * (size_t)n) == hipSuccess;
-}
-#endif
