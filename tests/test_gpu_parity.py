@@ -381,3 +381,33 @@ def test_lane_kernel_end_derivs_invalid_and_tail(solver, oracle, M):
         for a in range(3):
             ref = Rb[b, :, a]
             assert np.abs(Cb[b, :, a] - ref).max() <= TOL * max(np.abs(ref).max(), 1e-300)
+
+
+@pytest.mark.parametrize("method", [0, 2])
+def test_two_streams_share_handle_scratch(solver, method):
+    """Two ragged solves of one handle issued back to back on two different streams
+    (the second call re-uploads the handle's trajectory permutation and, for
+    the band method, reuses its U slabs while the first call's kernels may still run).
+    The handle orders them on the GPU; both must equal their one-stream host solves."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    so1, W1, T1 = S.ragged_batch(6000, 2, 16, seed=21)
+    so2, W2, T2 = S.ragged_batch(3001, 2, 16, seed=22)  # different B and grouping
+    solver.set_method(method)
+    try:
+        R1, _, w1 = solver.solve(so1, W1, T1)
+        R2, _, w2 = solver.solve(so2, W2, T2)
+        assert w1 == 0 and w2 == 0
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        dev = [(torch.from_numpy(so).cuda(), torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda(),
+                torch.zeros((int(so[-1]), 3, 8), dtype=torch.float64, device="cuda"))
+               for so, W, T in ((so1, W1, T1), (so2, W2, T2))]
+        torch.cuda.synchronize()
+        solver.solve_batch_device(so1, *dev[0], stream=s1.cuda_stream)
+        solver.solve_batch_device(so2, *dev[1], stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        solver.set_method(METHOD_REDUCED)
+    assert np.array_equal(dev[0][3].cpu().numpy(), R1)
+    assert np.array_equal(dev[1][3].cpu().numpy(), R2)
