@@ -205,12 +205,18 @@ __device__ __forceinline__ gdouble* opaque(gdouble* p) {
     return p;
 }
 
-// Entering row k+WR, column-parallel and branch-free: lane j assembles register slot j,
-// lanes 0..2 also slots 16..18 and lanes 3..5 the right-hand sides (slots 19..21).  The
-// row's block, offset and right-hand-side source are wave-uniform (scalar unit).  Same
-// entries as row_entry.
+// Entering row k+WR from its structural nonzeros (at most NE = 10 per row of the
+// interleaved KKT): lanes 0..10 zero the row's 22 slots, then lane j < NE writes
+// nonzero j of the row's pattern (coef * V_i[idx] at column r + d) and lanes NE..NE+2 the
+// right-hand sides.  The row's block, offset and right-hand-side source are wave-uniform
+// (scalar unit).  Same entries as row_entry (the list is built from the same table).
+constexpr int NE = 10;                  // structural nonzeros per row, at most
+constexpr int NPAT = 4 * NOFF;          // (variant, row offset) patterns
+
+__host__ __device__ constexpr int pack_ent(int coef, int d, int idx) { return (coef << 10) | ((d + KL) << 5) | idx; }
+
 template <int M, bool HAS_ED, int R>
-__device__ __forceinline__ void enter_row(int k, int j, const int* desc, const double* val, const double* w,
+__device__ __forceinline__ void enter_row(int k, int j, const int* ents, const double* val, const double* w,
                                           const double* ed, double* E) {
     constexpr int N = 14 * M + 2;
     const int r = k + WR;
@@ -231,33 +237,28 @@ __device__ __forceinline__ void enter_row(int k, int j, const int* desc, const d
         }
     }
     const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
-    const int* drow = desc + (vv * NOFF + o + 4) * WC + KL;
-    const double* vrow = val + i * VAL;
-    auto entry = [&](int c) {
-        const int d = c - r;
-        const bool inb = live_r && c < N && d >= -KL && d <= KL;
-        const int de = drow[min(max(d, -KL), KL)];
-        const double m = (double)(de >> 5) * vrow[de & 31];
-        return inb ? m : 0.0;
-    };
-    const double e0 = entry(enter_col<R>(k, j));
-    const double e1 = entry(enter_col<R>(k, min(j + QG, WC - 1)));
-    const int ax = min(max(j - 3, 0), 2);
+    if (j < UW / 2) reinterpret_cast<double2*>(E)[j] = make_double2(0.0, 0.0);
+    const int e = ents[(vv * NOFF + o + 4) * NE + min(j, NE - 1)];
+    const int d = ((e >> 5) & 31) - KL;
+    const double v = (double)(e >> 10) * val[i * VAL + (e & 31)];
+    int t = R + WR + d;  // register slot of column r + d (in [k+1, k+19])
+    t -= (t >= WC) ? WC : 0;
+    const int ax = min(max(j - NE, 0), 2);
     const double rw = w[max(wr, 0) * 3 + ax];
     const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
-    const double rhs = (live_r && wr >= 0) ? rw : ((HAS_ED && live_r && eb >= 0) ? re : 0.0);
-    E[j] = e0;
-    if (j < 6) E[QG + j] = (j < 3) ? e1 : rhs;
+    const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
+    const bool put = live_r && ((j < NE) ? (e != 0) : (j < NE + 3));
+    if (put) E[(j < NE) ? t : WC + ax] = (j < NE) ? v : rhs;
 }
 
 template <int M, bool HAS_ED, int R>
 __device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double (&rh)[3], int& pos, bool& sing,
-                                         double* P, double* E, gdouble* U, const int* desc, const double* val,
+                                         double* P, double* E, gdouble* U, const int* ents, const double* val,
                                          const double* w, const double* ed) {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int j = opaque(j0);
-    enter_row<M, HAS_ED, R>(k, j, desc, val, w, ed, E);
+    enter_row<M, HAS_ED, R>(k, j, ents, val, w, ed, E);
     // pivot search in column k (register R) over the window lanes: DPP max of |a|, then
     // the lowest position among the maxima
     const double cv = u[R];
@@ -405,6 +406,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
                                                        int32_t* __restrict__ status, double* __restrict__ scratch) {
     constexpr int N = 14 * M + 2;
     __shared__ int s_desc[NDESC];                            // entry pattern of the interleaved KKT
+    __shared__ int s_ents[NPAT * NE];                        // the same, as per-row nonzero lists
     __shared__ double s_val[QW][QT][M * VAL];                // V_i = [1, T_i^0..T_i^7, 2Q_i] per segment
     __shared__ double s_w[QW][QT][(M + 1) * 3];              // waypoints
     __shared__ double s_ed[QW][QT][HAS_ED ? 18 : 1];         // end derivatives
@@ -416,6 +418,15 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     for (int q = threadIdx.x; q < NDESC; q += QW * W64) {
         const int vv = q / (NOFF * WC), rem = q - vv * NOFF * WC, o = rem / WC - 4, d = rem % WC - KL;
         s_desc[q] = desc_entry(vv, o, d);
+    }
+    for (int q = threadIdx.x; q < NPAT; q += QW * W64) {
+        const int vv = q / NOFF, o = q % NOFF - 4;
+        int n = 0;
+        for (int d = -KL; d <= KL; ++d) {
+            const int de = desc_entry(vv, o, d);
+            if (de != 0 && n < NE) s_ents[q * NE + n++] = pack_ent(de >> 5, d, de & 31);
+        }
+        for (; n < NE; ++n) s_ents[q * NE + n] = 0;
     }
     __syncthreads();
     const int wave_id = blockIdx.x * QW + wv;
@@ -484,7 +495,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         bool sing = false;
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) row_step<M, HAS_ED, R>(k0 + R, j, u, rh, pos, sing, P, E, U, s_desc, val, w, ed);
+    if (k0 + R < N) row_step<M, HAS_ED, R>(k0 + R, j, u, rh, pos, sing, P, E, U, s_ents, val, w, ed);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
