@@ -286,8 +286,18 @@ __device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double 
         for (int a = 0; a < 3; ++a) P[WC + a] = rh[a];
     }
     __builtin_amdgcn_wave_barrier();
-    double p[UW];
-    {
+    // U row k to the slab: lane j < 11 copies 16 B of it
+    if (j < UW / 2) {
+        const double2 v = reinterpret_cast<const double2*>(P)[j];
+        gdouble* Uk = U + (size_t)k * UW + 2 * j;
+        Uk[0] = v.x;
+        Uk[1] = v.y;
+    }
+    // rank-1 update of the other window rows (only they read the pivot row: the LDS
+    // pipe, not the VALU, is the tighter resource); column k leaves (register R becomes
+    // column k+19, zero outside the entering row)
+    if (win && !piv) {
+        double p[UW];
         const double2* Pd = reinterpret_cast<const double2*>(P);
 #pragma unroll
         for (int q = 0; q < UW / 2; ++q) {
@@ -295,21 +305,12 @@ __device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double 
             p[2 * q] = v.x;
             p[2 * q + 1] = v.y;
         }
-        // U row k to the slab: lane j < 11 copies 16 B of it
-        if (j < UW / 2) {
-            const double2 v = Pd[j];
-            gdouble* Uk = U + (size_t)k * UW + 2 * j;
-            Uk[0] = v.x;
-            Uk[1] = v.y;
-        }
+        const double l = cv * p[0];
+#pragma unroll
+        for (int d = 1; d < WC; ++d) u[(R + d) % WC] = fma(-l, p[d], u[(R + d) % WC]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) rh[a] = fma(-l, p[WC + a], rh[a]);
     }
-    // rank-1 update of the other window rows; column k leaves (register R becomes
-    // column k+19, zero outside the entering row)
-    const double l = (win && !piv) ? cv * p[0] : 0.0;
-#pragma unroll
-    for (int d = 1; d < WC; ++d) u[(R + d) % WC] = fma(-l, p[d], u[(R + d) % WC]);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) rh[a] = fma(-l, p[WC + a], rh[a]);
     u[R] = 0.0;
     if (pos == k) pos = cp;  // interchange: the row at position k takes the pivot's position
     if (piv) {               // the pivot lane takes row k+WR
