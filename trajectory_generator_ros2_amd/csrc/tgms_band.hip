@@ -20,7 +20,7 @@
 // sides: 176 B) goes to a per-trajectory slab; back substitution (back_step) streams
 // the slab in reverse, a 16-B piece of a row per lane, as a DPP dot product.
 // Round 2's first mapping (a half-wavefront per trajectory, lane = window column) took
-// 2.50 ms per 65,536 at M = 10; this one 1.69 ms.
+// 2.50 ms per 65,536 at M = 10; this one 1.56 ms.
 #include <algorithm>
 
 #include "tgms_device.h"
