@@ -74,8 +74,8 @@ typedef enum tgms_method {
                                  pivoting LU, one workgroup per trajectory (M <= 10) */
     TGMS_METHOD_BAND_KKT = 2   /* the same KKT and LU with partial pivoting, in the
                                  segment-interleaved order where it is banded (kl = ku = 9);
-                                 the structurally-zero entries are skipped, half a wavefront
-                                 per trajectory, M <= TGMS_MAX_SEGMENTS.  Its U rows live in a
+                                 the structurally-zero entries are skipped, a 16-lane row of
+                                 a wavefront per trajectory, M <= TGMS_MAX_SEGMENTS.  Its U rows live in a
                                  handle-owned scratch slab (calls of one handle on different
                                  streams are serialised on the GPU) */
 } tgms_method;

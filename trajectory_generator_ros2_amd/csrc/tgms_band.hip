@@ -1,5 +1,5 @@
 // tgms_band.hip — TGMS_METHOD_BAND_KKT: the survey's literal KKT,
-// LU with partial pivoting, one half-wavefront per trajectory.
+// LU with partial pivoting, a 16-lane row of a wavefront per trajectory.
 //
 // The KKT [[2Q, A^T],[A, 0]] (N = 14M+2) is ordered segment-interleaved:
 //   [start rows (4) | c_0 (8) | knot-1 rows (6) | c_1 (8) | ... | c_{M-1} (8) | end rows (4)]
