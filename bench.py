@@ -143,7 +143,7 @@ def cpu_baseline(B: int, M: int, target_s: float):
     t1 = time.perf_counter()
     O.solve_batch(so[:1025], W[: 1024 * (M + 1)], T[: 1024 * M], None, O.KKT_C4, 1)
     dense_1 = 1024 / (time.perf_counter() - t1)
-    return {"value": red_rate, "unit": "trajectories/s", "cores": threads, "kind": "port",
+    return {"value": red_rate, "unit": "trajectories/s", "cores": threads, "kind": "cpu_restatement",
             "what": "cpu_restatement (reference has no solver): oracle/minsnap_oracle.c, fp64, OpenMP",
             "cores_detail": cores, "cpu_model": _cpu_model(),
             "value_1core": red_1, "dense_kkt_value": dense_rate, "dense_kkt_value_1core": dense_1,
@@ -422,12 +422,223 @@ def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
                          "algorithmic_bytes_per_launch": nbytes, "kernel": "k_sample"}}
 
 
+def resolve_topology(gpus: int, env: dict, visible: int):
+    """How `--gpus N` maps onto processes and devices.
+
+    * under a launcher (WORLD_SIZE in the environment, e.g. torch.distributed.run): one
+      rank per GPU, and WORLD_SIZE must equal N;
+    * no launcher: ONE process drives N devices (0..N-1) -- the shape of the reference's
+      caller, one C++ process holding one Trajectory (TrajectoryGenerator.hpp:83) --
+      and N must not exceed the visible devices.
+    Returns ("ranks", world, rank, local) or ("process", N, 0, 0); raises SystemExit
+    with a message otherwise."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} ranks but --gpus {gpus}; "
+                             f"start one rank per GPU (--nproc-per-node {gpus}) or drop the launcher")
+        return "ranks", world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+    if gpus > visible:
+        raise SystemExit(f"bench.py: --gpus {gpus} but only {visible} HIP device(s) are visible; "
+                         f"refusing to report a {gpus}-GPU line from fewer GPUs")
+    return "process", gpus, 0, 0
+
+
+class Lane:
+    """One device's share of the headline: its handle, its `sets` batches, its launch
+    stream (the device's current torch stream) and the captured graph of K steps."""
+
+    def __init__(self, dev: int, gpu_index: int, B: int, M: int, sets: int, method: int):
+        import torch
+        from trajectory_generator_ros2_amd import synthetic as S
+        from trajectory_generator_ros2_amd.solver import Solver
+        self.dev, self.B, self.M = dev, B, M
+        with torch.cuda.device(dev):
+            self.solver = Solver(dev, method)
+            self.bufs = []
+            for i in range(sets):
+                _, Wi, Ti = S.uniform_batch(B, M, seed=S.SEED + gpu_index + 7919 * i)
+                if i == 0:
+                    self.W, self.T = Wi, Ti
+                self.bufs.append((torch.from_numpy(Wi).to(dev), torch.from_numpy(Ti).to(dev),
+                                  torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev),
+                                  torch.full((B,), -1, dtype=torch.int32, device=dev)))
+            self.stream = torch.cuda.current_stream(dev)
+            self.ev0 = torch.cuda.Event(enable_timing=True)
+            self.ev1 = torch.cuda.Event(enable_timing=True)
+        self.graph = None
+        sp = self.stream.cuda_stream
+        _solve = self.solver._L.tgms_solve_uniform_device
+        self._args = [(self.solver._h, B, M, b[0].data_ptr(), b[1].data_ptr(), None, b[2].data_ptr(),
+                       b[3].data_ptr(), ctypes.c_void_p(sp)) for b in self.bufs]
+        self._solve = _solve
+
+    def step(self, k: int):
+        st = self._solve(*self._args[k % len(self._args)])
+        if st != 0:
+            raise RuntimeError(f"tgms_solve_uniform_device on device {self.dev}: status {st}: "
+                               f"{self.solver.last_error()}")
+
+    def capture(self, K: int):
+        """The K steps captured once into a HIP graph (thread-local capture: another
+        thread -- the RCCL watchdog at N > 1 ranks -- may keep making HIP calls)."""
+        import torch
+        with torch.cuda.device(self.dev):
+            cap = torch.cuda.Stream(device=self.dev)
+            cap.wait_stream(self.stream)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
+                for k in range(K):
+                    dWk, dTk, dCk, dSk = self.bufs[k % len(self.bufs)]
+                    self.solver.solve_uniform_device(self.B, self.M, dWk, dTk, dCk, dSk, stream=cap.cuda_stream)
+            self.stream.wait_stream(cap)
+            g.replay()  # warm replay (graph upload)
+            torch.cuda.synchronize(self.dev)
+        self.graph = g
+
+    def failures(self) -> int:
+        return sum(int((b[3] != 0).sum().item()) for b in self.bufs)
+
+
+def _timed_multi(fn, dev0_stream, reps: int, devs):
+    """Run fn() `reps` times after one warm call; wall clock between synchronisations of
+    every device of the process, plus HIP events on device 0's stream."""
+    import torch
+    fn()
+    for d in devs:
+        torch.cuda.synchronize(d)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(dev0_stream)
+    for _ in range(reps):
+        fn()
+    e1.record(dev0_stream)
+    for d in devs:
+        torch.cuda.synchronize(d)
+    wall = (time.perf_counter() - t0) / reps * 1e3
+    return wall, e0.elapsed_time(e1) / reps
+
+
+def config4_full_line(devs, ref_solver, reps=3, B_total=1048576, M=10):
+    """Config 4 at its stated size through the library's own multi-GPU path: ONE
+    tgms_solve_batch_multi_device call over len(devs) devices solves 1,048,576 x M = 10
+    (2.0 GB of coefficients) held on device 0: contiguous shards, device 0 scatters the
+    other shards' inputs piece by piece over RCCL and gathers their coefficients back
+    while the next piece is solved (tgms_capi.hip multi_run).  At one device the shard
+    is the whole batch, solved in place.  Check: slices at the start, the end and every
+    shard boundary re-solved by a single-device handle, bit for bit."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver, plan_shards
+    n = len(devs)
+    so, W, T = S.uniform_batch(B_total, M)
+    with torch.cuda.device(0):
+        dso = torch.from_numpy(so).cuda(0)
+        dW = torch.from_numpy(W.reshape(-1, 3)).cuda(0)
+        dT = torch.from_numpy(T.reshape(-1)).cuda(0)
+        dC = torch.empty((B_total * M, 3, 8), dtype=torch.float64, device="cuda:0")
+        dS = torch.full((B_total,), -1, dtype=torch.int32, device="cuda:0")
+        stream = torch.cuda.current_stream(0)
+        mh = Solver(device_count=n)
+        try:
+            wall, ev = _timed_multi(lambda: mh.solve_batch_multi_device(so, dso, dW, dT, dC, dS,
+                                                                        stream=stream.cuda_stream),
+                                    stream, reps, devs)
+        finally:
+            mh.close()
+        bad = int((dS != 0).sum().item())
+        bounds = [int(b) for b in plan_shards(so, n)]
+        chk, k = [], 512
+        for b in sorted(set([0, B_total - k] + [max(0, c - k // 2) & ~1 for c in bounds[1:-1]])):
+            ref = torch.empty((k * M, 3, 8), dtype=torch.float64, device="cuda:0")
+            ref_solver.solve_uniform_device(k, M, dW[b * (M + 1):(b + k) * (M + 1)],
+                                            dT[b * M:(b + k) * M], ref, stream=stream.cuda_stream)
+            torch.cuda.synchronize(0)
+            chk.append(bool(torch.equal(ref, dC[b * M:(b + k) * M])))
+    gathered = B_total - (bounds[1] - bounds[0])
+    return {"workload": f"config4 (full): {B_total} trajectories x {M} segments in one tgms_solve_batch_multi_device "
+                        f"call over {n} device(s), inputs and the 2.0 GB of coefficients on device 0",
+            "devices": n, "ms_per_call": wall, "ms_per_call_events_dev0": ev,
+            "trajectories_per_s": B_total / (wall * 1e-3),
+            "shard_bounds": bounds, "trajectories_gathered_over_rccl": gathered,
+            "bytes_gathered": gathered * M * 24 * 8, "status_failures": bad,
+            "bit_equal_single_device_slices": all(chk), "slices_checked": len(chk)}
+
+
+def config5_full_line(devs, reps=3, B_total=1048576, iters=10, k_T=1.0, eta=0.1):
+    """Config 5 at its stated size through the library's multi-GPU path: ONE
+    tgms_refine_loop_multi_device call over len(devs) devices: 1,048,576 ragged
+    trajectories (M ~ U{2..16}), `iters` time-refinement steps + the final solve, the
+    shards cost-balanced (tgms_plan_shards), times / costs / coefficients gathered to
+    device 0.  The times are reset from a device copy before every call (outside the
+    events)."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver
+    n = len(devs)
+    so, W, T = S.ragged_batch(B_total, 2, 16)
+    B, Sg = len(so) - 1, int(so[-1])
+    with torch.cuda.device(0):
+        d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda(0)
+        dso, dW, T0 = d(so), d(W), d(T)
+        dT = torch.empty_like(T0)
+        dC = torch.empty((Sg, 3, 8), dtype=torch.float64, device="cuda:0")
+        dcost = torch.empty((B,), dtype=torch.float64, device="cuda:0")
+        dst = torch.full((B,), -1, dtype=torch.int32, device="cuda:0")
+        stream = torch.cuda.current_stream(0)
+        mh = Solver(device_count=n)
+        try:
+            def run():
+                dT.copy_(T0)
+                mh.refine_loop_multi_device(so, dso, dW, dT, k_T, eta, iters, dC, dcost, dst,
+                                            stream=stream.cuda_stream)
+            wall, _ = _timed_multi(run, stream, reps, devs)
+            # events around the call alone
+            run()
+            torch.cuda.synchronize(0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            evs = []
+            for _ in range(reps):
+                dT.copy_(T0)
+                e0.record(stream)
+                mh.refine_loop_multi_device(so, dso, dW, dT, k_T, eta, iters, dC, dcost, dst,
+                                            stream=stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize(0)
+                evs.append(e0.elapsed_time(e1))
+        finally:
+            mh.close()
+        bad = int((dst != 0).sum().item())
+        finite = bool(torch.isfinite(dcost).all().item())
+    ms = sorted(evs)[len(evs) // 2]
+    return {"workload": f"config5 (full): {B_total} ragged trajectories (M~U{{2..16}}, {Sg} segments), {iters} "
+                        f"refinement steps + final solve in one tgms_refine_loop_multi_device call over {n} "
+                        f"device(s)",
+            "devices": n, "ms_per_call": ms, "ms_per_call_wall_incl_time_reset": wall,
+            "trajectories_per_s": B / (ms * 1e-3), "segments": Sg, "k_T": k_T, "eta": eta,
+            "status_failures": bad, "costs_finite": finite}
+
+
+def _side(name, fn):
+    """A side line that fails reports its error instead of ending the run."""
+    try:
+        return fn()
+    except Exception as exc:  # noqa: BLE001 -- recorded in the JSON line
+        print(f"bench: side line {name} failed: {type(exc).__name__}: {exc}", file=sys.stderr)
+        return {"error": f"{type(exc).__name__}: {exc}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of the run.  Under torch.distributed.run: one rank per GPU (WORLD_SIZE must equal "
+                         "it).  Without a launcher: one process drives devices 0..N-1 (one handle and stream "
+                         "per device for the headline; the library's multi-GPU handle for the config-4/5 lines)")
     ap.add_argument("--backend", default="nccl",
-                    help="process-group backend at N > 1 (nccl = RCCL; gloo only to rehearse the N > 1 control "
-                         "flow with several ranks on one GPU)")
+                    help="process-group backend at N > 1 ranks (nccl = RCCL; gloo only to rehearse the N > 1 "
+                         "control flow with several ranks on one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
@@ -441,11 +652,13 @@ def main():
     ap.add_argument("--band-steps", type=int, default=5, help="steps of the band-KKT side line (0: skip)")
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
-    ap.add_argument("--config5", type=int, default=1, help="config-5 side line (ragged + refinement): 1/0")
+    ap.add_argument("--config5", type=int, default=1,
+                    help="config-5 side lines (ragged + refinement: one GPU's share, and the full batch): 1/0")
     ap.add_argument("--cache-resident", type=int, default=1,
                     help="side line: the same batch every launch (its 148.6 MB stay in the Infinity Cache): 1/0")
     ap.add_argument("--config4", type=int, default=1,
-                    help="config-4 side line (131,072/GPU, pipelined RCCL gather to rank 0 when N > 1): 1/0")
+                    help="config-4 side lines (131,072/GPU shard; the full 1,048,576 batch through the "
+                         "library's multi-GPU call, or a per-rank RCCL gather under a launcher): 1/0")
     ap.add_argument("--node-line", type=int, default=1, help="config-1 node-path latency side line: 1/0")
     ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
@@ -454,53 +667,43 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    mode, n_total, rank, local = resolve_topology(args.gpus, os.environ, torch.cuda.device_count())
+    world = n_total if mode == "ranks" else 1          # processes
+    if mode == "ranks" and world > 1:
         local = local % max(torch.cuda.device_count(), 1) if args.backend == "gloo" else local
         torch.cuda.set_device(local)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.backend)
+        devs = [local]
+    elif mode == "ranks":
+        devs = [0]
     else:
-        torch.cuda.set_device(0)
+        devs = list(range(n_total))
+    torch.cuda.set_device(devs[0])
 
     from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
-    from trajectory_generator_ros2_amd import synthetic as S
-    from trajectory_generator_ros2_amd.solver import Solver
 
     B, M, sets = args.batch, args.segments, max(1, args.sets)
-    dev = torch.cuda.current_device()
-    solver = Solver(dev, METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
-    # this rank's shard of the job: `sets` independent batches of independent
-    # trajectories (set 0: seed + rank, as every side line uses)
-    bufs = []
-    for i in range(sets):
-        _, Wi, Ti = S.uniform_batch(B, M, seed=S.SEED + rank + 7919 * i)
-        if i == 0:
-            W, T = Wi, Ti
-        bufs.append((torch.from_numpy(Wi).to(dev), torch.from_numpy(Ti).to(dev),
-                     torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev),
-                     torch.full((B,), -1, dtype=torch.int32, device=dev)))
-    dW, dT, dC, dS = bufs[0]
-    stream = torch.cuda.current_stream()
+    method = METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED
+    # this process's devices, each with its own shard of the job: `sets` independent
+    # batches of independent trajectories (set 0: seed + GPU index, as every side line uses)
+    lanes = [Lane(d, rank if mode == "ranks" else d, B, M, sets, method) for d in devs]
+    torch.cuda.set_device(devs[0])
+    lane0 = lanes[0]
+    solver, dev, stream = lane0.solver, lane0.dev, lane0.stream
+    W, T = lane0.W, lane0.T
+    dW, dT, dC, dS = lane0.bufs[0]
     sp = stream.cuda_stream
-
-    # the timed launches with their arguments bound once (the C-ABI call and nothing else)
-    _solve = solver._L.tgms_solve_uniform_device
-    _args = [(solver._h, B, M, b[0].data_ptr(), b[1].data_ptr(), None, b[2].data_ptr(), b[3].data_ptr(),
-              ctypes.c_void_p(sp)) for b in bufs]
-
-    def step(k):
-        st = _solve(*_args[k % sets])
-        if st != 0:
-            raise RuntimeError(f"tgms_solve_uniform_device: status {st}: {solver.last_error()}")
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def sync_all():
+        for L in lanes:
+            torch.cuda.synchronize(L.dev)
 
     def all_ranks(x: float, op):
         if world == 1:
@@ -509,68 +712,67 @@ def main():
         dist.all_reduce(t, op=op)
         return float(t.item())
 
-    for k in range(max(args.warmup, sets)):
-        step(k)
-    torch.cuda.synchronize()
-    assert all(int((b[3] != 0).sum().item()) == 0 for b in bufs), "solver reported failures"
+    for L in lanes:
+        for k in range(max(args.warmup, sets)):
+            L.step(k)
+    sync_all()
+    assert all(L.failures() == 0 for L in lanes), "solver reported failures"
 
     K = args.steps
-    # The K steps are captured once into a HIP graph (torch.cuda.CUDAGraph over the
-    # library's launches) and replayed as one submission, so a slow or busy host cannot
-    # starve the GPU between ~30 us launches; every step is still one full solve of a
-    # batch.  HIP events on the launch stream bracket the timed region; the average
-    # launch duration is their elapsed time / K.  --graph 0: K Python-level launches.
-    # Every rank times the same launch mode: if capture fails on any rank, all fall back.
-    graph, capture_error = None, None
+    # The K steps are captured once into a HIP graph per device (torch.cuda.CUDAGraph over
+    # the library's launches) and replayed as one submission, so a slow or busy host
+    # cannot starve the GPU between ~30 us launches; every step is still one full solve
+    # of a batch.  HIP events on each device's launch stream bracket its timed region;
+    # the average launch duration is their elapsed time / K.  --graph 0: K Python-level
+    # launches.  Every rank times the same launch mode: if capture fails anywhere, all
+    # fall back.
+    capture_error = None
     if args.graph:
         try:
-            cap = torch.cuda.Stream()
-            cap.wait_stream(stream)
-            graph = torch.cuda.CUDAGraph()
-            # thread-local capture: other threads (the RCCL process group's watchdog at
-            # N > 1) may keep making HIP calls while this thread captures
-            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
-                for k in range(K):
-                    dWk, dTk, dCk, dSk = bufs[k % sets]
-                    solver.solve_uniform_device(B, M, dWk, dTk, dCk, dSk, stream=cap.cuda_stream)
-            stream.wait_stream(cap)
-            graph.replay()  # warm replay (graph upload)
-            torch.cuda.synchronize()
+            for L in lanes:
+                L.capture(K)
         except Exception as exc:  # capture unsupported here: time the Python loop instead
             capture_error = f"{type(exc).__name__}: {exc}"
             print(f"bench: HIP graph capture failed ({capture_error}); timing the launch loop", file=sys.stderr)
-            graph = None
-            torch.cuda.synchronize()
-        if all_ranks(1.0 if graph is not None else 0.0, dist.ReduceOp.MIN if world > 1 else None) < 1.0:
-            graph = None  # some rank could not capture: every rank times the launch loop
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+            for L in lanes:
+                L.graph = None
+            sync_all()
+        ok = 1.0 if all(L.graph is not None for L in lanes) else 0.0
+        if all_ranks(ok, dist.ReduceOp.MIN if world > 1 else None) < 1.0:
+            for L in lanes:
+                L.graph = None  # some rank could not capture: every rank times the launch loop
+    graphed = all(L.graph is not None for L in lanes)
     barrier()
-    torch.cuda.synchronize()
+    sync_all()
     t0 = time.perf_counter()
-    ev0.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        for k in range(K):
-            step(k)
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    for L in lanes:  # every device's K steps issued from this one thread, then all run
+        L.ev0.record(L.stream)
+        if graphed:
+            with torch.cuda.device(L.dev):
+                L.graph.replay()
+        else:
+            for k in range(K):
+                L.step(k)
+        L.ev1.record(L.stream)
+    sync_all()
     barrier()
     el = all_ranks(time.perf_counter() - t0, dist.ReduceOp.MAX if world > 1 else None)
-    launch_ms = ev0.elapsed_time(ev1) / K
-    launch_ms_max = all_ranks(launch_ms, dist.ReduceOp.MAX if world > 1 else None)
-    launch_ms_min = all_ranks(launch_ms, dist.ReduceOp.MIN if world > 1 else None)
-    assert all(int((b[3] != 0).sum().item()) == 0 for b in bufs), "solver reported failures"
-    launch_mode = "hip_graph_of_K_steps" if graph is not None else "python_loop"
-    del graph
+    launch_each = [L.ev0.elapsed_time(L.ev1) / K for L in lanes]
+    launch_ms_max = all_ranks(max(launch_each), dist.ReduceOp.MAX if world > 1 else None)
+    launch_ms_min = all_ranks(min(launch_each), dist.ReduceOp.MIN if world > 1 else None)
+    assert all(L.failures() == 0 for L in lanes), "solver reported failures"
+    launch_mode = "hip_graph_of_K_steps" if graphed else "python_loop"
+    for L in lanes:
+        L.graph = None
 
-    per_launch = launch_stats(solver, B, M, bufs, stream)
+    per_launch = launch_stats(solver, B, M, lane0.bufs, stream)
     cache_res = None
     if args.cache_resident and args.method == "reduced":
-        cache_res = cache_resident_line(solver, B, M, bufs[0], stream)
-    # the side lines use set 0 only
-    del bufs, _args
+        cache_res = cache_resident_line(solver, B, M, lane0.bufs[0], stream)
+    # the side lines use device 0's set 0 only
+    for L in lanes:
+        L.bufs = L.bufs[:1]
+        L._args = L._args[:1]
     torch.cuda.empty_cache()
 
     # dense-KKT side line (the survey's literal formulation), same inputs, same GPU
@@ -589,10 +791,10 @@ def main():
         dms = e0.elapsed_time(e1) / args.dense_steps
         diff = (dC2 - dC).abs().amax(dim=(1, 3)) / dC.abs().amax(dim=(1, 3)).clamp_min(1e-300)
         gfl = dense_flops_per_traj(M) * B / (dms * 1e-3) / 1e12
-        dense = {"value": B / (dms * 1e-3) * world, "ms_per_step": dms,
+        dense = {"value": B / (dms * 1e-3), "ms_per_step": dms,
                  "fp64_tflops_algorithmic": gfl, "fp64_peak_tflops": FP64_PEAK_TFS,
                  "max_rel_diff_vs_reduced": float(diff.max().item())}
-        solver.set_method(METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED)
+        solver.set_method(method)
         del dC2
 
     # band-KKT side line: the same literal KKT and partial-pivoting LU in the order in
@@ -612,20 +814,24 @@ def main():
         assert int((dS != 0).sum().item()) == 0, "band KKT reported failures"
         bms = e0.elapsed_time(e1) / args.band_steps
         diff = (dC3 - dC).abs().amax(dim=(1, 3)) / dC.abs().amax(dim=(1, 3)).clamp_min(1e-300)
-        band = {"value": B / (bms * 1e-3) * world, "ms_per_step": bms,
+        band = {"value": B / (bms * 1e-3), "ms_per_step": bms,
                 "fp64_tflops_algorithmic": band_flops_per_traj(M) * B / (bms * 1e-3) / 1e12,
                 "flops_per_traj": band_flops_per_traj(M), "fp64_peak_tflops": FP64_PEAK_TFS,
                 "max_rel_diff_vs_reduced": float(diff.max().item())}
         solver.set_method(METHOD_REDUCED)
         del dC3
 
-    config5 = None
+    config5 = config5_full = None
     if args.config5 and M == 10:
         config5 = config5_line(solver, dev, stream, world, rank)
+        if world == 1:
+            config5_full = _side("config5_full", lambda: config5_full_line(devs))
 
-    config4 = None
+    config4 = config4_full = None
     if args.config4 and M == 10:
         config4 = config4_line(solver, M, dev, stream, world, rank)
+        if world == 1:
+            config4_full = _side("config4_full", lambda: config4_full_line(devs, solver))
 
     sampler = None
     if args.sample_traj > 0:
@@ -650,12 +856,17 @@ def main():
         achieved = bpl / (launch_ms_max * 1e-3) / 1e9
         key = f"B{B}_M{M}_{args.method}_sets{sets}"
         traffic = load_traffic(key)
-        value = world * B * K / el
+        value = n_total * B * K / el
+        if mode == "ranks":
+            parallelism = f"shard{n_total}: one rank per GPU (independent trajectories, no collective)"
+        else:
+            parallelism = (f"shard{n_total}: one process, one handle + stream + graph per device, launched from one "
+                           f"thread (independent trajectories, no collective)")
         line = {
             "metric": "min-snap trajectories/sec (10-seg, order-7, 3-axis) at batch=65k; 1/2/4/8 GPU",
             "value": value,
             "unit": "trajectories/s",
-            "n_gpus": world,
+            "n_gpus": n_total,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": el / K * 1e3,
@@ -663,14 +874,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md 8(d): seed 20251015+rank(+7919 i for batch i), room-bound uniform "
+            "data": "synthetic (SURVEY.md 8(d): seed 20251015+GPU index(+7919 i for batch i), room-bound uniform "
                     "waypoints, T=clip(|dw|/1m/s,0.5,10), rest-to-rest)",
             "config": {"workload": f"config3: {B} trajectories/GPU x {M} segments, order 7, 3 axes, "
                                    f"coefficients [traj][seg][axis][8] fp64 in HBM; a fresh batch every step "
                                    f"({sets} batches rotated, {sets * bpl / 1e6:.0f} MB per GPU)",
                        "batch_per_gpu": B, "segments": M, "sets": sets, "method": args.method,
-                       "launch": launch_mode,
-                       "parallelism": f"shard{world} (independent trajectories, no collective)"},
+                       "launch": launch_mode, "processes": world, "devices_per_process": len(devs),
+                       "parallelism": parallelism},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
@@ -689,7 +900,9 @@ def main():
             "band_kkt": band,
             "sampler": sampler,
             "config4": config4,
+            "config4_full": config4_full,
             "config5": config5,
+            "config5_full": config5_full,
             "host_path": host,
             "node_config1": node,
         }
@@ -697,7 +910,8 @@ def main():
             line["config"]["graph_capture_error"] = capture_error
         print(json.dumps(line), flush=True)
     barrier()
-    solver.close()
+    for L in lanes:
+        L.solver.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -30,6 +30,14 @@
  *     them on the GPU with an event (each waits for the previous one's work);
  *     fp64 device arrays must be 16-byte aligned (TGMS_ERR_INVALID_ARG otherwise;
  *     hipMalloc allocations are, a slice at an odd element offset is not);
+ *   - HIP-graph capture: uniform solves (tgms_solve_uniform_device, any method, and
+ *     tgms_solve_batch_device / tgms_refine_*_device on a uniform batch) may be
+ *     captured into a caller's graph.  Inside a capture the scratch event handshake
+ *     is skipped, so a graph holding band-KKT launches must be replayed in stream
+ *     order with the handle's other band calls.  Calls that upload a host-side launch
+ *     plan or grow scratch at call time (ragged batches, tgms_refine_loop_device,
+ *     the multi-GPU calls, a band slab that must grow) return TGMS_ERR_UNSUPPORTED
+ *     while their stream is capturing;
  *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
  *     TGMS_ERR_NO_DEVICE.
  *

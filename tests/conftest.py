@@ -96,3 +96,72 @@ def check_spline_properties(so, W, T, C, atol_pos=1e-8, rtol_cont=1e-7):
     for k in range(1, 4):
         assert np.abs(C[first, :, k]).max() == 0.0
         assert np.abs(_deriv(C[last], Tt[last], k)).max() <= atol_pos
+
+
+
+def check_spline_properties_torch(so, W, T, C, atol_pos=1e-8, rtol_cont=1e-7, chunk=1 << 20):
+    """check_spline_properties for a batch held in torch tensors (fp64, any device:
+    the 1,048,576-trajectory configs are checked where they live).  Same properties
+    and tolerances: c0 = start waypoint (1e-12), p(T) = end waypoint (atol_pos),
+    derivatives 1..6 continuous at every interior knot (rtol_cont x (max|right| + 1)
+    over a chunk of `chunk` segments), v = a = j = 0 at both ends.  Plain torch
+    elementwise arithmetic, independent of the kernels under test."""
+    import torch
+    dev = C.device
+    so = torch.as_tensor(np.asarray(so, dtype=np.int64), device=dev)
+    W = W.reshape(-1, 3)
+    T = T.reshape(-1)
+    C = C.reshape(-1, 3, 8)
+    B = so.numel() - 1
+    S = C.shape[0]
+    Ms = so[1:] - so[:-1]
+    rows = torch.arange(S, device=dev) + torch.repeat_interleave(torch.arange(B, device=dev), Ms)
+    last = torch.zeros(S, dtype=torch.bool, device=dev)
+    last[so[1:] - 1] = True
+    first = so[:-1]
+    assert float((C[..., 0] - W[rows]).abs().max()) <= 1e-12
+    assert float(C[first][:, :, 1:4].abs().max()) == 0.0
+    j = torch.arange(8, device=dev, dtype=torch.float64)
+    fact = [1.0, 1.0, 2.0, 6.0, 24.0, 120.0, 720.0]
+    for s0 in range(0, S, chunk):
+        s1 = min(S, s0 + chunk)
+        t = T[s0:s1, None]
+        cs = C[s0:s1]
+        inner = ~last[s0:s1]
+        if s1 == S:
+            inner[-1] = False
+        nxt = C[s0 + 1:min(S, s1 + 1)]
+        for k in range(0, 7):
+            f = torch.ones(8, device=dev, dtype=torch.float64)
+            for q in range(k):
+                f = f * (j - q)
+            f = torch.where(j >= k, f, torch.zeros_like(f))
+            G = f * torch.pow(t, torch.clamp(j - k, min=0))  # [n, 8]
+            val = (cs * G[:, None, :]).sum(-1)               # [n, 3]: k-th derivative at T
+            if k == 0:
+                assert float((val - W[rows[s0:s1] + 1]).abs().max()) <= atol_pos
+                continue
+            if 1 <= k <= 3:
+                lv = val[last[s0:s1]]
+                assert lv.numel() == 0 or float(lv.abs().max()) <= atol_pos, k
+            n_in = int(inner.sum())
+            if n_in:
+                idx = torch.nonzero(inner).reshape(-1)
+                right = fact[k] * nxt[idx][:, :, k]
+                left = val[idx]
+                scale = float(right.abs().max()) + 1.0
+                assert float((left - right).abs().max()) <= rtol_cont * scale, k
+
+
+def check_spline_properties_chunked(so, W, T, C, chunk=65536, **kw):
+    """check_spline_properties over a large CSR batch in host chunks of `chunk`
+    trajectories (every trajectory is checked; the temporaries stay ~chunk-sized)."""
+    so = np.asarray(so, dtype=np.int64)
+    W = np.asarray(W).reshape(-1, 3)
+    T = np.asarray(T).reshape(-1)
+    C = np.asarray(C).reshape(-1, 3, 8)
+    B = so.shape[0] - 1
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        s0, s1 = int(so[lo]), int(so[hi])
+        check_spline_properties(so[lo:hi + 1] - s0, W[s0 + lo:s1 + hi + 1], T[s0:s1], C[s0:s1], **kw)

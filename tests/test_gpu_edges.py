@@ -104,3 +104,25 @@ def test_largest_m_at_swarm_scale(solver, oracle):
         R, _ = oracle.solve_batch(sub_so, W[sl].reshape(-1, 3), T[sl].reshape(-1), None, oracle.REDUCED)
         C = out[METHOD_BAND_KKT][sl].reshape(-1, 3, 8).cpu().numpy()
         assert batch_rel_err(sub_so, C, R) <= TOL
+
+
+@pytest.mark.parametrize("t_small", [1e-100, 1e-200])
+def test_breakdown_writes_exact_zeros(solver, method, t_small):
+    """A segment time so small that its powers underflow makes the KKT numerically
+    singular (the oracle's LU reports TGMS_ERR_SINGULAR from 1e-100 on).  Whatever a
+    method reports for such a trajectory, a failed one must come out as exact zeros
+    (never stale or NaN data from the caller's buffer), and its neighbours must be
+    untouched by it."""
+    from trajectory_generator_ros2_amd import ERR_NONFINITE, ERR_SINGULAR, OK
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(3, 2, seed=77)
+    W, T = W.reshape(-1, 3), T.reshape(-1).copy()
+    T[3] = t_small  # trajectory 1, second segment
+    C = np.full((6, 3, 8), np.nan)
+    st = np.full(3, -1, np.int32)
+    _, st, worst = solver.solve(so, W, T, out=(C, st))
+    assert st[0] == OK and st[2] == OK
+    assert st[1] in (OK, ERR_SINGULAR, ERR_NONFINITE)
+    if st[1] == ERR_SINGULAR:
+        assert (C[2:4] == 0.0).all(), C[2:4]
+    assert np.isfinite(C[[0, 1, 4, 5]]).all()

@@ -106,3 +106,131 @@ def test_multi_handle_single_device_calls_and_errors(multi):
         assert multi.solve_multi(so11, W11.reshape(-1, 3), T11.reshape(-1))[2] == ERR_UNSUPPORTED
     finally:
         multi.set_method(METHOD_REDUCED)
+
+
+def _self_gather_handle(extra_env=None):
+    """A one-device multi handle whose shard goes through the RCCL pipeline."""
+    from trajectory_generator_ros2_amd.solver import Solver
+    env = {"TGMS_MULTI_SELF_GATHER": "1", **(extra_env or {})}
+    old = {k: os.environ.pop(k, None) for k in env}
+    os.environ.update(env)
+    try:
+        return Solver(device_count=1)
+    finally:
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("meth", ["band", "dense"])
+def test_multi_pipeline_other_methods(solver, meth):
+    """The literal-KKT methods through the piece pipeline: their sub-handles allocate
+    their own scratch (band slabs); bit-equal to the single-device call, ragged."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    m = METHOD_BAND_KKT if meth == "band" else METHOD_DENSE_KKT
+    so, W, T = S.ragged_batch(3000, 1, 16 if meth == "band" else 10, seed=44)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so), d(W), d(T)
+    S_ = int(so[-1])
+    mh = _self_gather_handle()
+    try:
+        solver.set_method(m)
+        mh.set_method(m)
+        ref = torch.empty((S_, 3, 8), dtype=torch.float64, device="cuda")
+        solver.solve_batch_device(so, dso, dW, dT, ref)
+        got = torch.full_like(ref, float("nan"))
+        st = torch.full((len(so) - 1,), -1, dtype=torch.int32, device="cuda")
+        mh.solve_batch_multi_device(so, dso, dW, dT, got, st)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        assert int(st.abs().sum()) == 0
+    finally:
+        solver.set_method(METHOD_REDUCED)
+        mh.close()
+
+
+def test_multi_back_to_back_async_calls(solver):
+    """back-to-back asynchronous multi calls on one handle with no
+    host synchronisation between them, batch sizes large -> small -> large and a
+    refinement call in between (its gathers read the times right after the waypoint
+    region), M mixes changing every call.  Every result must equal the single-device
+    solve of the same batch bit for bit: a later call's plan upload must not land in
+    the workspace while the previous call's gathers still read it."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    mh = _self_gather_handle()
+    try:
+        jobs = [("solve", S.ragged_batch(20000, 1, 16, seed=50)),
+                ("solve", S.ragged_batch(700, 3, 5, seed=51)),
+                ("refine", S.ragged_batch(9000, 2, 16, seed=52)),
+                ("solve", S.uniform_batch(15000, 10, seed=53)),
+                ("solve", S.ragged_batch(20000, 8, 16, seed=54))]
+        res = []
+        for kind, (so, W, T) in jobs:  # all issued, nothing synchronised
+            W, T = W.reshape(-1, 3), T.reshape(-1)
+            B, S_ = len(so) - 1, int(so[-1])
+            dso, dW, dT = d(so), d(W), d(T.copy())
+            dC = torch.full((S_, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+            dst = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+            if kind == "solve":
+                mh.solve_batch_multi_device(so, dso, dW, dT, dC, dst)
+                res.append((kind, so, dso, dW, dT, dC, dst, None))
+            else:
+                dcost = torch.full((B,), float("nan"), dtype=torch.float64, device="cuda")
+                mh.refine_loop_multi_device(so, dso, dW, dT, 1.0, 0.1, 10, dC, dcost, dst)
+                res.append((kind, so, dso, dW, dT, dC, dst, dcost))
+        torch.cuda.synchronize()
+        for kind, so, dso, dW, dT, dC, dst, dcost in res:
+            assert int(dst.abs().sum()) == 0, kind
+            if kind == "solve":
+                ref = torch.empty_like(dC)
+                solver.solve_batch_device(so, dso, dW, dT, ref)
+                torch.cuda.synchronize()
+                assert torch.equal(dC, ref), (kind, len(so) - 1)
+            else:
+                T0 = [T for k, (s, W, T) in jobs if k == "refine"][0]
+                rT = d(T0.copy())
+                rC = torch.empty_like(dC)
+                rc = torch.empty_like(dcost)
+                solver.refine_loop_device(so, dso, dW, rT, 1.0, 0.1, 10, rC, rc)
+                torch.cuda.synchronize()
+                assert torch.equal(dT, rT) and torch.equal(dC, rC) and torch.equal(dcost, rc)
+    finally:
+        mh.close()
+
+
+@pytest.mark.parametrize("hook", ["piece:1", "group:2", "piece:0"])
+def test_multi_error_path_leaves_handle_usable(solver, hook):
+    """a multi call that fails after planning -- a piece's dispatch
+    (after earlier pieces' gathers were queued) or inside an open gather group -- reports
+    TGMS_ERR_DEVICE, closes every RCCL group it opened and drains what it queued; the
+    next multi call on the same handle is then bit-equal to the single-device call."""
+    import torch
+    from trajectory_generator_ros2_amd import ERR_DEVICE, TgmsError
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(6000, 2, 16, seed=60)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so), d(W), d(T)
+    S_ = int(so[-1])
+    mh = _self_gather_handle({"TGMS_MULTI_FAIL": hook})
+    try:
+        got = torch.full((S_, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+        with pytest.raises(TgmsError) as ei:
+            mh.solve_batch_multi_device(so, dso, dW, dT, got)
+        assert ei.value.status == ERR_DEVICE and "injected" in mh.last_error()
+        assert torch.cuda.current_device() == 0
+        ref = torch.empty_like(got)
+        solver.solve_batch_device(so, dso, dW, dT, ref)
+        for _ in range(2):  # the hook fired once; the handle works again
+            got.fill_(float("nan"))
+            st = torch.full((len(so) - 1,), -1, dtype=torch.int32, device="cuda")
+            mh.solve_batch_multi_device(so, dso, dW, dT, got, st)
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+            assert int(st.abs().sum()) == 0
+    finally:
+        mh.close()

@@ -115,17 +115,35 @@ tgms_status ensure_ws(tgms_handle* h, size_t bytes) {
     return TGMS_OK;
 }
 
-// Order `stream` after every earlier user of the handle's device scratch.
+// True while `stream` is being captured into a HIP graph.
+bool capturing(hipStream_t stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Order `stream` after every earlier user of the handle's device scratch.  Inside a
+// caller's stream capture the handshake is skipped (an event recorded outside the
+// capture cannot order a graph's replays): a graph that holds band-KKT launches must
+// be replayed in stream order with the handle's other scratch users (include/tgms.h).
 tgms_status scratch_acquire(tgms_handle* h, hipStream_t stream) {
-    if (h->scratch_pending) TGMS_HIP(h, hipStreamWaitEvent(stream, h->scratch_ev, 0));
+    if (h->scratch_pending && !capturing(stream)) TGMS_HIP(h, hipStreamWaitEvent(stream, h->scratch_ev, 0));
     return TGMS_OK;
 }
 
 // The work just enqueued on `stream` is the scratch's latest user.
 tgms_status scratch_release(tgms_handle* h, hipStream_t stream) {
+    if (capturing(stream)) return TGMS_OK;
     TGMS_HIP(h, hipEventRecord(h->scratch_ev, stream));
     h->scratch_pending = true;
     return TGMS_OK;
+}
+
+tgms_status no_capture(tgms_handle* h, hipStream_t stream, const char* what) {
+    if (!capturing(stream)) return TGMS_OK;
+    return set_err(h, TGMS_ERR_UNSUPPORTED,
+                   std::string(what) + " cannot be captured into a HIP graph: it uploads a launch plan from the "
+                                       "handle's host staging (or grows device scratch) at call time; capture "
+                                       "uniform solves, or issue this call outside the capture");
 }
 
 tgms_status ensure_loop_ws(tgms_handle* h, size_t bytes) {
@@ -212,6 +230,8 @@ tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m,
     tgms_status s = check_offsets(h, B, h_so, max_m, &p->counts, &p->uniform_m);
     if (s != TGMS_OK || B == 0) return s;
     if (p->uniform_m > 0) return TGMS_OK;
+    s = no_capture(h, stream, "a ragged batch");
+    if (s != TGMS_OK) return s;
     s = upload_plan(h, B, h_so, p->counts, &p->starts, stream);
     p->d_perm = h->d_perm;
     return s;
@@ -317,6 +337,8 @@ tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream) {
     }
     const size_t need = tgms::band_scratch_bytes(m_max, h->band_grid);
     if (need <= h->band_cap) return TGMS_OK;
+    tgms_status s = no_capture(h, stream, "a band-KKT call that grows the handle's slab");
+    if (s != TGMS_OK) return s;
     if (h->d_band) {
         TGMS_HIP(h, hipStreamSynchronize(stream));
         TGMS_HIP(h, hipDeviceSynchronize());
@@ -593,6 +615,10 @@ struct tgms_multi_ctx {
     std::vector<std::vector<hipEvent_t>> ev_piece;
     hipEvent_t ev_start = nullptr, ev_end = nullptr;
     bool self_gather = false;  // device 0's shard through the RCCL pipeline too (tests on one GPU)
+    // error-path test hook (TGMS_MULTI_FAIL="piece:k" or "group:k", read at
+    // tgms_create_multi, fires once): the dispatch of piece k, or the gather group of
+    // piece k right after ncclGroupStart, reports a device error
+    int fail_kind = 0, fail_piece = -1;  // kind 1: piece dispatch, 2: inside the gather group
 };
 
 namespace {
@@ -607,6 +633,41 @@ tgms_status nccl_err(tgms_handle* h, ncclResult_t e, const char* where) {
         ncclResult_t n_ = (call);                             \
         if (n_ != ncclSuccess) return nccl_err(h, n_, #call); \
     } while (0)
+
+// An RCCL group opened by start() is closed on every exit of the scope: an early
+// return from inside ncclGroupStart() .. ncclGroupEnd() would otherwise leave the
+// thread's group depth raised, and every later RCCL call of the thread deferred into
+// a group that never ends.  (After a failed send/recv, ncclGroupEnd reports the
+// group's error and launches none of its operations.)
+struct NcclGroup {
+    const RcclApi& r;
+    bool open = false;
+    explicit NcclGroup(const RcclApi& api) : r(api) {}
+    ncclResult_t start() {
+        const ncclResult_t e = r.group_start();
+        open = e == ncclSuccess;
+        return e;
+    }
+    ncclResult_t end() {
+        open = false;
+        return r.group_end();
+    }
+    ~NcclGroup() {
+        if (open) (void)r.group_end();
+    }
+    NcclGroup(const NcclGroup&) = delete;
+    NcclGroup& operator=(const NcclGroup&) = delete;
+};
+
+// The calling thread's HIP device, restored on every exit of a multi-device call.
+struct DeviceRestore {
+    int dev = 0;
+    bool ok = false;
+    DeviceRestore() { ok = hipGetDevice(&dev) == hipSuccess; }
+    ~DeviceRestore() {
+        if (ok) (void)hipSetDevice(dev);
+    }
+};
 
 void destroy_multi(tgms_multi_ctx* m) {
     if (!m) return;
@@ -653,8 +714,36 @@ void piece_plan(const int32_t* so_rebased, int32_t n, int max_m, Plan* p, int32_
 }
 
 // The multi-GPU pipeline (see the section comment).  Arrays in `a` live on device 0
-// and are ordered on `ustream` (a device-0 stream).
+// and are ordered on `ustream` (a device-0 stream).  Stream roles per device d:
+//   sm[d]  plan upload, scatter receive (d = 0: every send too), gathers
+//   sc[d]  the pieces' solves (waits for the scatter; the gathers wait for it)
+// The plan upload goes on sm[d], so it is ordered after the previous call's gathers,
+// which read the same workspace (a later call's plan block may overlap the previous
+// call's piece outputs).
+tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustream);
+
+// Drain every stream of the pipeline: after a failure nothing the call already queued
+// may still write into the caller's buffers once the error has been returned.
+void multi_drain(tgms_multi_ctx* m) {
+    for (int d = 0; d < m->n; ++d) {
+        if (hipSetDevice(d) != hipSuccess) continue;
+        if (m->sm[d]) (void)hipStreamSynchronize(m->sm[d]);
+        if (m->sc[d]) (void)hipStreamSynchronize(m->sc[d]);
+    }
+}
+
 tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
+    DeviceRestore restore;  // the caller's device on every return
+    const tgms_status s = multi_enqueue(h, a, ustream);
+    if (s != TGMS_OK) {
+        multi_drain(h->multi);
+        (void)hipSetDevice(0);
+        (void)hipStreamSynchronize(ustream);
+    }
+    return s;
+}
+
+tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
     tgms_multi_ctx* m = h->multi;
     const int n = m->n;
     const bool refine = a.job == MultiJob::Refine;
@@ -721,17 +810,25 @@ tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
             p.plan.d_perm = reinterpret_cast<const int32_t*>(m->dws[d] + p.oPerm);
         }
         if (plan_bytes) {
-            TGMS_HIP(h, hipMemcpyAsync(m->dws[d], m->pin[d], plan_bytes, hipMemcpyHostToDevice, m->sc[d]));
-            TGMS_HIP(h, hipEventRecord(m->ev_up[d], m->sc[d]));
+            // on sm[d]: after the previous call's gathers out of this workspace
+            TGMS_HIP(h, hipMemcpyAsync(m->dws[d], m->pin[d], plan_bytes, hipMemcpyHostToDevice, m->sm[d]));
+            TGMS_HIP(h, hipEventRecord(m->ev_up[d], m->sm[d]));
             m->up_pending[d] = true;
         }
     }
+    // Everything a send/recv below is given was planned above: the pieces' ranges lie
+    // inside the batch, their workspaces are allocated, and the peers are 0..n-1.
+    for (int d = 0; d < n; ++d)
+        for (const Piece& p : pieces[d])
+            if (!m->dws[d] || p.lo < 0 || p.hi > a.B || p.s0 < 0 || p.s1 > a.h_so[a.B])
+                return set_err(h, TGMS_ERR_DEVICE, "internal: multi-GPU piece plan out of range");
     // device 0: the caller's inputs are ready on ustream
     TGMS_HIP(h, hipSetDevice(0));
     TGMS_HIP(h, hipEventRecord(m->ev_start, ustream));
     TGMS_HIP(h, hipStreamWaitEvent(m->sm[0], m->ev_start, 0));
     // scatter: every piece's inputs from device 0 into its device's workspace
-    TGMS_NCCL(h, m->r.group_start());
+    NcclGroup scatter(m->r);
+    TGMS_NCCL(h, scatter.start());
     for (int d = 0; d < n; ++d)
         for (const Piece& p : pieces[d]) {
             char* w = m->dws[d];
@@ -745,7 +842,7 @@ tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
                 TGMS_NCCL(h, m->r.recv(w + p.oED, ne, ncclFloat64, 0, m->comm[d], m->sm[d]));
             }
         }
-    TGMS_NCCL(h, m->r.group_end());
+    TGMS_NCCL(h, scatter.end());
     for (int d = 0; d < n; ++d) {
         if (pieces[d].empty()) continue;
         TGMS_HIP(h, hipSetDevice(d));
@@ -804,13 +901,22 @@ tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
             } else {
                 s = dispatch(hd, p.plan, p.n(), so_p, Wp, Tp, EDp, Cp, Stp, m->sc[d]);
             }
+            if (s == TGMS_OK && m->fail_kind == 1 && m->fail_piece == k) {
+                m->fail_kind = 0;  // fires once
+                s = set_err(hd, TGMS_ERR_DEVICE, "injected failure of a piece's dispatch (TGMS_MULTI_FAIL)");
+            }
             if (s != TGMS_OK) return hd == h ? s : set_err(h, s, std::string("device ") + std::to_string(d) + ": " +
                                                                  tgms_last_error(hd));
             TGMS_HIP(h, hipEventRecord(m->ev_piece[d][k], m->sc[d]));
             TGMS_HIP(h, hipStreamWaitEvent(m->sm[d], m->ev_piece[d][k], 0));
         }
         if (!any) break;
-        TGMS_NCCL(h, m->r.group_start());
+        NcclGroup gather(m->r);
+        TGMS_NCCL(h, gather.start());
+        if (m->fail_kind == 2 && m->fail_piece == k) {
+            m->fail_kind = 0;  // fires once: leaves the (still empty) group to the guard
+            return set_err(h, TGMS_ERR_DEVICE, "injected failure inside a gather group (TGMS_MULTI_FAIL)");
+        }
         for (int d = 0; d < n; ++d) {
             if (k >= (int)pieces[d].size()) continue;
             const Piece& p = pieces[d][k];
@@ -832,7 +938,7 @@ tgms_status multi_run(tgms_handle* h, const MultiArgs& a, hipStream_t ustream) {
                 }
             }
         }
-        TGMS_NCCL(h, m->r.group_end());
+        TGMS_NCCL(h, gather.end());
     }
     TGMS_HIP(h, hipSetDevice(0));
     TGMS_HIP(h, hipEventRecord(m->ev_end, m->sm[0]));
@@ -846,6 +952,12 @@ tgms_status create_multi_ctx(tgms_handle* h, int n) {
     m->n = n;
     const char* sg = std::getenv("TGMS_MULTI_SELF_GATHER");
     m->self_gather = sg && sg[0] == '1';
+    if (const char* f = std::getenv("TGMS_MULTI_FAIL")) {  // error-path test hook
+        int k = -1;
+        if (sscanf(f, "piece:%d", &k) == 1) m->fail_kind = 1;
+        else if (sscanf(f, "group:%d", &k) == 1) m->fail_kind = 2;
+        m->fail_piece = k;
+    }
     std::string err;
     if (!m->r.load(&err)) return set_err(h, TGMS_ERR_DEVICE, err);
     m->comm.assign(n, nullptr);
@@ -1221,6 +1333,8 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    s = no_capture(h, st, "tgms_refine_loop_device (it captures and replays its own graph)");
+    if (s != TGMS_OK) return s;
     const size_t S = (size_t)h_so[B];
     s = ensure_loop_ws(h, align256(S * 8));
     if (s == TGMS_OK) s = scratch_acquire(h, st);
@@ -1403,6 +1517,8 @@ tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32
     if (s != TGMS_OK || B == 0) return s;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
+    s = no_capture(h, static_cast<hipStream_t>(stream), "a multi-GPU call");
+    if (s != TGMS_OK) return s;
     MultiArgs a;
     a.job = MultiJob::Solve;
     a.B = B;
@@ -1413,9 +1529,7 @@ tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32
     a.dED = dED;
     a.dC = dC;
     a.dSt = dSt;
-    s = multi_run(h, a, static_cast<hipStream_t>(stream));
-    (void)hipSetDevice(h->device);
-    return s;
+    return multi_run(h, a, static_cast<hipStream_t>(stream));
 }
 
 tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32_t* h_so, const int32_t* d_so,
@@ -1432,6 +1546,8 @@ tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32
     if (s != TGMS_OK || B == 0) return s;
     if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
+    s = no_capture(h, static_cast<hipStream_t>(stream), "a multi-GPU call");
+    if (s != TGMS_OK) return s;
     MultiArgs a;
     a.job = MultiJob::Refine;
     a.B = B;
@@ -1446,9 +1562,7 @@ tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32
     a.k_T = k_T;
     a.eta = eta;
     a.iters = iters;
-    s = multi_run(h, a, static_cast<hipStream_t>(stream));
-    (void)hipSetDevice(h->device);
-    return s;
+    return multi_run(h, a, static_cast<hipStream_t>(stream));
 }
 
 tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* so, const double* waypoints,

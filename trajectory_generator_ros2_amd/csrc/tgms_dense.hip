@@ -278,6 +278,12 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     }
 
     // ---- x_k = b'_{p_k} / a_{p_k k}: the right-hand-side owners write the coefficients ----
+    // A singular matrix stopped the elimination early (uniformly: every thread read the
+    // same pivot), so rows never pivoted hold no position: the whole trajectory is
+    // written as exact zeros instead, as the band and lane kernels do on failure.
+    if (singular) {
+        for (int e = tid; e < 24 * M; e += GJ_T) C[s0 * 24 + e] = 0.0;
+    }
     double fin = 0.0;
 #pragma unroll
     for (int j = 0; j < CJ; ++j) {
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
                 const int k = pos[i];
-                if (k < n) {
+                if (k < n && !singular) {
                     const double x = singular ? 0.0 : a[i][j] * s_ipiv[k];
                     fin += x;
                     C[s0 * 24 + ((k >> 3) * 3 + ax) * 8 + (k & 7)] = valid ? x : 0.0;
