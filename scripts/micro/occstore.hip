@@ -27,14 +27,32 @@ __global__ __launch_bounds__(64) void k(const double2* __restrict__ in, double2*
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = seed + lane + j;
     const double2* src = in + w * in_per_wave;
-    for (size_t i = lane; i < in_per_wave; i += 64) {
-        const double2 v = src[i];
-        acc[i & 7] += v.x + v.y;
-    }
-    for (int i = 0; i < fma; ++i) {
+    // every load of the wave's slice in flight at once (up to 24 per lane per batch),
+    // as the lane kernel's LDS-DMA prologue issues them
+    for (size_t i0 = 0; i0 < in_per_wave; i0 += 24 * 64) {
+        double2 v[24];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fma(acc[j], 0.999999, 1e-9);
+        for (int q = 0; q < 24; ++q) {
+            const size_t i = i0 + q * 64 + lane;
+            v[q] = i < in_per_wave ? src[i] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < 24; ++q) acc[q & 7] += v[q].x + v[q].y;
     }
+    // 16 independent FMA chains (the lane kernel's forward sweep has ~3 x 3 x 3-deep
+    // independent work per knot)
+    double acc2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc2[j] = acc[j] * 0.5;
+    for (int i = 0; i < fma / 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[j] = __builtin_fma(acc[j], 0.999999, 1e-9);
+            acc2[j] = __builtin_fma(acc2[j], 0.999999, 1e-9);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += acc2[j];
     if (seed < -1e300) pin_lds[lane] = acc[0];  // never: keeps the LDS allocation
     double2* dst = out + w * out_per_wave;
     for (size_t i = lane, q = 0; i < out_per_wave; i += 64, ++q) dst[i] = make_double2(acc[q & 7], acc[(q + 1) & 7]);
@@ -52,7 +70,7 @@ int main() {
     (void)hipEventCreate(&e1);
     // fp64 FMA wave-instructions per 64 trajectories: 0 (pure streaming) and ~3,300
     // (the lane kernel's measured FP64 work, r02_fp64pmc_summary), and twice that
-    for (int pass = 0; pass < 2; ++pass)
+    for (int pass = 0; pass < 1; ++pass)
         for (int read : {0, 1})
             for (int prefix : {0, 3328, 6656})
                 for (int wps : {1, 2, 4, 8})

@@ -571,7 +571,8 @@ __device__ __forceinline__ void row_coeffs(const LaneView& L, bool right, int e,
 
 template <int M, class Out>
 __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
-                                          const double (&xs)[3], const double (&xe)[3], bool has_r) {
+                                          const double (&xs)[3], const double (&xe)[3], bool has_r,
+                                          bool zero = false) {
     const double ws = L.w(e, a), we = L.w(e + 1, a);
     const double w0 = right ? we : ws, w1 = right ? ws : we;
     // the odd lane runs the segment backwards: physical start = virtual knot e+1, with P
@@ -596,7 +597,9 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
         o.J[e] += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
     } else {
-        const double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
+        double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
         if constexpr (__is_same(Out, OutBuf))
             stage_axis(o, c, a, out_step(o, e), has_r);
         else
@@ -624,6 +627,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     MARK(ax_factor);
     AxFactors<M> Fa;
     ax_factor<M>(Fa, L, right);
+    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const bool valid = get_valid(valid_src);
     MARK(ax_axisloop);
     double fin = 0.0;
@@ -739,14 +743,13 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #pragma unroll
                 for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
             }
-            if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR);
+            if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR, !spd_pair);
         }
         MARK(ax_emit);
         SCHED_FENCE();
-        emit_axis<M, Out>(O, L, right, 0, a, u0, Y[0], 0 < nR);
+        emit_axis<M, Out>(O, L, right, 0, a, u0, Y[0], 0 < nR, !spd_pair);
     }
     MARK(ax_end);
-    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
     if (!spd_pair) return TGMS_ERR_SINGULAR;
@@ -757,12 +760,13 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 // Emit one segment (virtual knots 0, 1 with derivatives xs, xe [derivative][axis]).
 template <int M, class Out>
 __device__ __forceinline__ void emit_all_axes(const Out& O, const LaneView& L, bool right,
-                                              const double (&xs)[3][3], const double (&xe)[3][3], bool has_r) {
+                                              const double (&xs)[3][3], const double (&xe)[3][3], bool has_r,
+                                              bool zero = false) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const double s3[3] = {xs[0][a], xs[1][a], xs[2][a]};
         const double e3[3] = {xe[0][a], xe[1][a], xe[2][a]};
-        emit_axis<M, Out>(O, L, right, 0, a, s3, e3, has_r);
+        emit_axis<M, Out>(O, L, right, 0, a, s3, e3, has_r, zero);
     }
 }
 
@@ -810,7 +814,8 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
                 ldl3_solve(f, y[0][a], y[1][a], y[2][a], x[0][a], x[1][a], x[2][a]);
                 fin += (x[0][a] + x[1][a]) + x[2][a];
             }
-            emit_all_axes<M, Out>(O, L, right, u0, x, true);
+            const bool spd2 = spd && (pair_swap(spd ? 1.0 : 0.0) != 0.0);
+            emit_all_axes<M, Out>(O, L, right, u0, x, true, !spd2);
         }
         const bool spd_pair = spd && (pair_swap(spd ? 1.0 : 0.0) != 0.0);
         const double fin_pair = fin + pair_swap(fin);
@@ -1807,26 +1812,33 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
 #pragma unroll
             for (int a = 0; a < 3; ++a) wfin = wfin && finite(u0[d][a]) && finite(uM[d][a]);
     }
-    // An invalid trajectory (non-finite input, T <= 0) comes out as exact zeros: its
-    // elimination vectors, end derivatives and waypoint row are zeroed (rare path).
+    // An invalid trajectory (non-finite input, T <= 0) or a failed factorisation comes
+    // out as exact zeros: its elimination vectors and factors, end derivatives,
+    // waypoint row and 1/T row (unit times) are zeroed (rare path).
     valid = valid && wfin;
-    if (__builtin_amdgcn_ballot_w64(!valid) != 0) {
-        if (!valid) {
+    const bool keep = valid && spd;
+    if (__builtin_amdgcn_ballot_w64(!keep) != 0) {
+        if (!keep) {
 #pragma unroll
             for (int q = 0; q < NW; ++q) Wl[q] = 0.0;
+#pragma unroll
+            for (int i = 0; i < M; ++i) Rl[i] = 1.0;
         }
 #pragma unroll
         for (int k = 0; k < NK; ++k)
 #pragma unroll
             for (int d = 0; d < 3; ++d)
 #pragma unroll
-                for (int a = 0; a < 3; ++a) g[k][d][a] = valid ? g[k][d][a] : 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    g[k][d][a] = keep ? g[k][d][a] : 0.0;
+                    if (k < NK - 1) G[k][d][a] = keep ? G[k][d][a] : 0.0;
+                }
 #pragma unroll
         for (int d = 0; d < 3; ++d)
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                u0[d][a] = valid ? u0[d][a] : 0.0;
-                uM[d][a] = valid ? uM[d][a] : 0.0;
+                u0[d][a] = keep ? u0[d][a] : 0.0;
+                uM[d][a] = keep ? uM[d][a] : 0.0;
             }
         wave_lds_sync();
     }
