@@ -74,3 +74,17 @@ def test_rccl_is_loaded_not_linked(lib):
     assert "rccl" not in deps
     strings = open(LIB_TGMS, "rb").read()
     assert b"librccl.so.1" in strings and b"ncclCommInitAll" in strings
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_plan_shards_uniform_fast_path(lib, method):
+    """Uniform batches take a closed-form path in the C planner (no per-trajectory
+    prefix); it must cut exactly where the general rule and shard.ragged_bounds do."""
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd.solver import plan_shards
+    for B, M in [(1048576, 10), (1048575, 10), (131072, 16), (999, 1), (5, 7), (1, 3), (3, 2)]:
+        so = (np.arange(B + 1, dtype=np.int64) * M).astype(np.int32)
+        for parts in (1, 2, 3, 4, 5, 7, 8, 13):
+            got = plan_shards(so, parts, method)
+            ref = SH.ragged_bounds(so, parts, method if method == 1 else 0)
+            np.testing.assert_array_equal(got, ref.astype(np.int32), err_msg=f"B={B} M={M} parts={parts}")

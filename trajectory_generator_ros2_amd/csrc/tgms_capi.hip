@@ -166,6 +166,17 @@ tgms_status check_offsets(tgms_handle* h, int32_t B, const int32_t* so, int max_
     if (!so) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets is NULL");
     if (so[0] != 0) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets[0] != 0");
     if (counts) counts->assign(max_m + 1, 0);
+    // uniform batches (the common large case): one vectorisable pass over the offsets
+    if (B > 0) {
+        const int32_t M0 = so[1] - so[0];
+        int32_t diff = 0;
+        for (int32_t b = 0; b < B; ++b) diff |= (so[b + 1] - so[b]) ^ M0;
+        if (diff == 0 && M0 >= 1 && M0 <= TGMS_MAX_SEGMENTS && M0 <= max_m) {
+            if (counts) (*counts)[M0] = B;
+            if (uniform_m) *uniform_m = M0;
+            return TGMS_OK;
+        }
+    }
     int um = -1;
     for (int32_t b = 0; b < B; ++b) {
         const int32_t M = so[b + 1] - so[b];
@@ -226,15 +237,21 @@ struct Plan {
     const int32_t* d_perm = nullptr;  // ragged: trajectory ids grouped by M (device)
 };
 
-tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m, Plan* p, hipStream_t stream) {
-    tgms_status s = check_offsets(h, B, h_so, max_m, &p->counts, &p->uniform_m);
-    if (s != TGMS_OK || B == 0) return s;
-    if (p->uniform_m > 0) return TGMS_OK;
-    s = no_capture(h, stream, "a ragged batch");
+// The plan of a batch whose offsets check_offsets already validated into p->counts /
+// p->uniform_m (one host pass per call): uploads the grouping of a ragged batch.
+tgms_status plan_upload(tgms_handle* h, int32_t B, const int32_t* h_so, Plan* p, hipStream_t stream) {
+    if (B == 0 || p->uniform_m > 0) return TGMS_OK;
+    tgms_status s = no_capture(h, stream, "a ragged batch");
     if (s != TGMS_OK) return s;
     s = upload_plan(h, B, h_so, p->counts, &p->starts, stream);
     p->d_perm = h->d_perm;
     return s;
+}
+
+tgms_status make_plan(tgms_handle* h, int32_t B, const int32_t* h_so, int max_m, Plan* p, hipStream_t stream) {
+    tgms_status s = check_offsets(h, B, h_so, max_m, &p->counts, &p->uniform_m);
+    if (s != TGMS_OK) return s;
+    return plan_upload(h, B, h_so, p, stream);
 }
 
 tgms_status ensure_aux(tgms_handle* h) {
@@ -543,10 +560,33 @@ struct RcclApi {
 // Contiguous cost-balanced shards of a CSR batch: the rule of shard.ragged_bounds
 // (trajectory_generator_ros2_amd/shard.py), step for step in the same fp64 arithmetic,
 // so the C++ and Python planners give identical bounds (tests/test_multi_host.py).
-void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* bounds) {
+void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* bounds, int uniform_m = 0) {
     bounds[0] = 0;
     if (B == 0) {
         for (int k = 1; k <= parts; ++k) bounds[k] = 0;
+        return;
+    }
+    if (uniform_m > 0) {
+        // every trajectory costs the same integer w, so the running sum is exactly
+        // (b + 1) w in fp64: the same cuts as the general rule below, by binary search
+        const double m = (double)uniform_m;
+        const double w = method == TGMS_METHOD_DENSE_KKT ? (14.0 * m + 2.0) * (14.0 * m + 2.0) * (14.0 * m + 2.0)
+                                                         : 2.0 + m;
+        const double total = (double)B * w;
+        int64_t prev = 0;
+        for (int k = 1; k < parts; ++k) {
+            const double target = (total * (double)k) / (double)parts;
+            int64_t lo = 0, hi = B;  // first b with (b + 1) w >= target
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if ((double)(mid + 1) * w < target) lo = mid + 1;
+                else hi = mid;
+            }
+            int64_t cut = std::max(lo + 1, prev);
+            prev = cut;
+            bounds[k] = (int32_t)std::min<int64_t>(cut, B);
+        }
+        bounds[parts] = B;
         return;
     }
     std::vector<double> c(B);
@@ -584,6 +624,7 @@ struct MultiArgs {
     int32_t* dSt = nullptr;
     double k_T = 0.0, eta = 0.0;
     int32_t iters = 0;
+    const Plan* checked = nullptr;  // the whole batch's validated counts / uniform M
 };
 
 // One piece of one device's shard: trajectories [lo, hi) of the batch, and the byte
@@ -749,17 +790,22 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
     const bool refine = a.job == MultiJob::Refine;
     const int max_m = refine ? TGMS_MAX_SEGMENTS : max_m_for(h);
     std::vector<int32_t> bounds(n + 1);
-    plan_shards(a.B, a.h_so, n, h->method, bounds.data());
+    const int um = a.checked ? a.checked->uniform_m : 0;
+    plan_shards(a.B, a.h_so, n, h->method, bounds.data(), um);
     // pieces of every device that goes through the RCCL pipeline
     std::vector<std::vector<Piece>> pieces(n);
     for (int d = 0; d < n; ++d) {
         if (d == 0 && !m->self_gather) continue;
         const int32_t lo = bounds[d], hi = bounds[d + 1];
         if (hi <= lo) continue;
-        std::vector<int32_t> so_l(hi - lo + 1);
-        for (int32_t b = lo; b <= hi; ++b) so_l[b - lo] = a.h_so[b] - a.h_so[lo];
         int32_t pb[MULTI_PIECES + 1];
-        plan_shards(hi - lo, so_l.data(), MULTI_PIECES, h->method, pb);
+        if (um > 0) {
+            plan_shards(hi - lo, nullptr, MULTI_PIECES, h->method, pb, um);
+        } else {
+            std::vector<int32_t> so_l(hi - lo + 1);
+            for (int32_t b = lo; b <= hi; ++b) so_l[b - lo] = a.h_so[b] - a.h_so[lo];
+            plan_shards(hi - lo, so_l.data(), MULTI_PIECES, h->method, pb);
+        }
         size_t plan_bytes = 0, off = 0;
         for (int k = 0; k < MULTI_PIECES; ++k) {
             if (pb[k + 1] <= pb[k]) continue;
@@ -856,7 +902,13 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
         tgms_status s = scratch_acquire(h, ustream);
         if (s != TGMS_OK) return s;
         Plan p0;
-        s = make_plan(h, b1, a.h_so, max_m, &p0, ustream);
+        if (a.checked && b1 == a.B) {  // the whole batch on device 0: validated already
+            p0.counts = a.checked->counts;
+            p0.uniform_m = a.checked->uniform_m;
+            s = plan_upload(h, b1, a.h_so, &p0, ustream);
+        } else {
+            s = make_plan(h, b1, a.h_so, max_m, &p0, ustream);
+        }
         if (s != TGMS_OK) return s;
         if (refine) {
             const size_t S0 = (size_t)a.h_so[b1];
@@ -1096,7 +1148,8 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
                              int32_t* status) {
     if (!h) return TGMS_ERR_INVALID_ARG;
     h->last_error.clear();
-    tgms_status s = check_offsets(h, B, so, max_m_for(h), nullptr, nullptr);
+    Plan plan;
+    tgms_status s = check_offsets(h, B, so, max_m_for(h), &plan.counts, &plan.uniform_m);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!waypoints || !seg_times || !coeffs)
@@ -1127,8 +1180,7 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
     s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    Plan plan;
-    s = make_plan(h, B, so, max_m_for(h), &plan, st);
+    s = plan_upload(h, B, so, &plan, st);
     if (s != TGMS_OK) return s;
     s = dispatch(h, plan, B, dSo, dW, dT, dED, dC, dSt, st);
     if (s == TGMS_OK) s = scratch_release(h, st);
@@ -1200,7 +1252,8 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
                                     const double* dED, double* dC, int32_t* dSt, void* stream) {
     if (!h) return TGMS_ERR_INVALID_ARG;
     h->last_error.clear();
-    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), nullptr, nullptr);
+    Plan plan;
+    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), &plan.counts, &plan.uniform_m);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
@@ -1208,8 +1261,7 @@ tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_
     hipStream_t st = static_cast<hipStream_t>(stream);
     s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    Plan plan;
-    s = make_plan(h, B, h_so, max_m_for(h), &plan, st);
+    s = plan_upload(h, B, h_so, &plan, st);
     if (s != TGMS_OK) return s;
     s = dispatch(h, plan, B, d_so, dW, dT, dED, dC, dSt, st);
     if (s != TGMS_OK) return s;
@@ -1239,7 +1291,8 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
     h->last_error.clear();
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
-    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    Plan plan;
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, &plan.counts, &plan.uniform_m);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT || !dT_out || dT_out == dT) return set_err(h, TGMS_ERR_INVALID_ARG, "bad device pointers");
@@ -1247,8 +1300,7 @@ tgms_status tgms_refine_batch_device(tgms_handle* h, int32_t B, const int32_t* h
     hipStream_t st = static_cast<hipStream_t>(stream);
     s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    Plan plan;
-    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
+    s = plan_upload(h, B, h_so, &plan, st);
     if (s != TGMS_OK) return s;
     s = dispatch_refine(h, plan, B, d_so, dW, dT, dED, k_T, eta, dT_out, d_cost, dSt, st);
     if (s != TGMS_OK) return s;
@@ -1263,7 +1315,8 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
     if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
-    s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    Plan plan;
+    s = check_offsets(h, B, so, TGMS_MAX_SEGMENTS, &plan.counts, &plan.uniform_m);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!waypoints || !seg_times) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times");
@@ -1296,8 +1349,7 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
     s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
-    Plan plan;
-    s = make_plan(h, B, so, TGMS_MAX_SEGMENTS, &plan, st);
+    s = plan_upload(h, B, so, &plan, st);
     if (s != TGMS_OK) return s;
     int cur = 0;
     s = refine_loop(h, plan, B, dSo, dW, dT, dED, k_T, eta, iters, coeffs ? dC : nullptr, dCost, dSt, st, &cur);
@@ -1327,7 +1379,8 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
     if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
-    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    Plan plan;
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, &plan.counts, &plan.uniform_m);
     if (s != TGMS_OK) return s;
     if (B == 0) return TGMS_OK;
     if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
@@ -1340,8 +1393,7 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (s == TGMS_OK) s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
     double* T[2] = {dT, h->d_loop_ws};
-    Plan plan;
-    s = make_plan(h, B, h_so, TGMS_MAX_SEGMENTS, &plan, st);
+    s = plan_upload(h, B, h_so, &plan, st);
     if (s != TGMS_OK) return s;
     auto body = [&](hipStream_t q) -> tgms_status {
         int cur = 0;
@@ -1501,9 +1553,12 @@ tgms_status tgms_plan_shards(int32_t B, const int32_t* so, int32_t parts, int me
     if (parts < 1 || !bounds || B < 0 || !so || so[0] != 0) return TGMS_ERR_INVALID_ARG;
     if (method != TGMS_METHOD_REDUCED && method != TGMS_METHOD_DENSE_KKT && method != TGMS_METHOD_BAND_KKT)
         return TGMS_ERR_INVALID_ARG;
-    for (int32_t b = 0; b < B; ++b)
+    int32_t M0 = B > 0 ? so[1] - so[0] : 0, diff = 0;
+    for (int32_t b = 0; b < B; ++b) {
         if (so[b + 1] - so[b] < 1) return TGMS_ERR_INVALID_ARG;
-    plan_shards(B, so, parts, method, bounds);
+        diff |= (so[b + 1] - so[b]) ^ M0;
+    }
+    plan_shards(B, so, parts, method, bounds, diff == 0 ? M0 : 0);
     return TGMS_OK;
 }
 
@@ -1513,13 +1568,15 @@ tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32
     if (!h) return TGMS_ERR_INVALID_ARG;
     if (!h->multi) return tgms_solve_batch_device(h, B, h_so, d_so, dW, dT, dED, dC, dSt, stream);
     h->last_error.clear();
-    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), nullptr, nullptr);
+    Plan checked;
+    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), &checked.counts, &checked.uniform_m);
     if (s != TGMS_OK || B == 0) return s;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);
     s = no_capture(h, static_cast<hipStream_t>(stream), "a multi-GPU call");
     if (s != TGMS_OK) return s;
     MultiArgs a;
+    a.checked = &checked;
     a.job = MultiJob::Solve;
     a.B = B;
     a.h_so = h_so;
@@ -1542,13 +1599,15 @@ tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32
     tgms_status s = check_refine_args(h, k_T, eta);
     if (s != TGMS_OK) return s;
     if (iters < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "iters < 0");
-    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, nullptr, nullptr);
+    Plan checked;
+    s = check_offsets(h, B, h_so, TGMS_MAX_SEGMENTS, &checked.counts, &checked.uniform_m);
     if (s != TGMS_OK || B == 0) return s;
     if (!d_so || !dW || !dT) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC, d_cost);
     s = no_capture(h, static_cast<hipStream_t>(stream), "a multi-GPU call");
     if (s != TGMS_OK) return s;
     MultiArgs a;
+    a.checked = &checked;
     a.job = MultiJob::Refine;
     a.B = B;
     a.h_so = h_so;
@@ -1571,7 +1630,8 @@ tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* so,
     if (!h) return TGMS_ERR_INVALID_ARG;
     if (!h->multi) return tgms_solve_batch(h, B, so, waypoints, seg_times, end_derivs, coeffs, status);
     h->last_error.clear();
-    tgms_status s = check_offsets(h, B, so, max_m_for(h), nullptr, nullptr);
+    Plan checked;
+    tgms_status s = check_offsets(h, B, so, max_m_for(h), &checked.counts, &checked.uniform_m);
     if (s != TGMS_OK || B == 0) return s;
     if (!waypoints || !seg_times || !coeffs)
         return set_err(h, TGMS_ERR_INVALID_ARG, "NULL waypoints/seg_times/coeffs");
@@ -1600,6 +1660,7 @@ tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* so,
     if (dED) TGMS_HIP(h, hipMemcpyAsync(dED, end_derivs, nED * 8, hipMemcpyHostToDevice, st));
     TGMS_HIP(h, hipMemcpyAsync(dSo, so, (size_t)(B + 1) * 4, hipMemcpyHostToDevice, st));
     MultiArgs a;
+    a.checked = &checked;
     a.B = B;
     a.h_so = so;
     a.d_so = dSo;

@@ -520,27 +520,30 @@ struct is_grad : std::false_type {};
 template <int NE>
 struct is_grad<GradAcc<NE>> : std::true_type {};
 
-__device__ __forceinline__ void seg_cost(double D, const double (&z)[6], double& Q, double& Qd) {
-    // z = (V0, A0, J0, V1, A1, J1); derivative orders 1,2,3,1,2,3
-    constexpr double KP[6] = {-50400, -10080, -840, -50400, 10080, -840};  // KH[4][b]
-    constexpr double KD[6][6] = {{25920, 5400, 480, 24480, -4680, 360},   {5400, 1200, 120, 4680, -840, 60},
-                                 {480, 120, 16, 360, -60, 4},             {24480, 4680, 360, 25920, -5400, 480},
-                                 {-4680, -840, -60, -5400, 1200, -120},   {360, 60, 4, 480, -120, 16}};
-    constexpr int S[6] = {1, 2, 3, 1, 2, 3};
-    double q = 100800.0 * D * D, qd = -7.0 * 100800.0 * D * D;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        double t = 2.0 * KP[a] * D, td = 2.0 * KP[a] * (S[a] - 7) * D;
-#pragma unroll
-        for (int b = 0; b < 6; ++b) {
-            t = __builtin_fma(KD[a][b], z[b], t);
-            td = __builtin_fma(KD[a][b] * (S[a] + S[b] - 7), z[b], td);
-        }
-        q = __builtin_fma(t, z[a], q);
-        qd = __builtin_fma(td, z[a], qd);
-    }
-    Q = q;
-    Qd = qd;
+
+// The same J and dJ/dT from the segment's scaled monomial data P4..P7 (c_k = r^(k-3) P_k)
+// instead of the Hermite data: with s = t / T the snap is r q(s),
+// q = 24 P4 + 120 P5 s + 360 P6 s^2 + 840 P7 s^3, so J = r Q with Q = P^T H P,
+// H_kl = a_k a_l / (k + l + 1) for k, l = 0..3 (a = 24, 120, 360, 840; H_33 = 100800, KH's position
+// entry).  P is linear in u = (D, V0, A0, J0, V1, A1, J1) whose entries carry r^3, r^2,
+// r, 1, r^2, r, 1, so dQ/dr = (2/r) P^T H P' with P' the same map applied to
+// (3D, 2V0, A0, 0, 2V1, A1, 0); dJ/dT = -r^2 dJ/dr = r^2 Qd with Qd = -(Q + 2 P'^T H P).
+// 47 FP64 operations per axis and segment instead of ~100 for the quadratic form in u
+// with KH (round 2; the P4..P7 are computed for the coefficients anyway).  The two agree
+// up to rounding (tests/test_refine_oracle.py pins the gradient on the CPU side).
+__device__ __forceinline__ void seg_cost_p(double D, double V0, double A0, double V1, double A1, double P4,
+                                           double P5, double P6, double P7, double& Q, double& Qd) {
+    const double Q4 = 105.0 * D - 40.0 * V0 - 5.0 * A0 - 30.0 * V1 + 2.5 * A1;
+    const double Q5 = -252.0 * D + 90.0 * V0 + 10.0 * A0 + 78.0 * V1 - 7.0 * A1;
+    const double Q6 = 210.0 * D - 72.0 * V0 - 7.5 * A0 - 68.0 * V1 + 6.5 * A1;
+    const double Q7 = -60.0 * D + 20.0 * V0 + 2.0 * A0 + 20.0 * V1 - 2.0 * A1;
+    const double H4 = 576.0 * P4 + 1440.0 * P5 + 2880.0 * P6 + 5040.0 * P7;
+    const double H5 = 1440.0 * P4 + 4800.0 * P5 + 10800.0 * P6 + 20160.0 * P7;
+    const double H6 = 2880.0 * P4 + 10800.0 * P5 + 25920.0 * P6 + 50400.0 * P7;
+    const double H7 = 5040.0 * P4 + 20160.0 * P5 + 50400.0 * P6 + 100800.0 * P7;
+    Q = P4 * H4 + P5 * H5 + P6 * H6 + P7 * H7;
+    const double G = Q4 * H4 + Q5 * H5 + Q6 * H6 + Q7 * H7;
+    Qd = -(Q + 2.0 * G);
 }
 
 // Coefficients of axis a of virtual segment e (virtual knots e, e+1 with derivatives
@@ -590,9 +593,8 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
     const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
     const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
     if constexpr (is_grad<Out>::value) {
-        const double z[6] = {V0, A0, j0, V1, A1, j1};
         double Q, Qd;
-        seg_cost(D, z, Q, Qd);
+        seg_cost_p(D, V0, A0, V1, A1, P4, P5, P6, P7, Q, Qd);
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
         o.J[e] += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
