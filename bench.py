@@ -152,12 +152,22 @@ def cpu_baseline(B: int, M: int, target_s: float):
                       f"{threads} OpenMP thread(s)"}
 
 
-def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_T=1.0, eta=0.1, reps=3):
-    """Config 5: a 1,048,576-trajectory ragged batch (M ~ U{2..16}) split over `world`
-    GPUs into contiguous cost-balanced shards (shard.ragged_bounds over 8 shards, the
-    configuration's GPU count, whatever N is); this rank solves shard `rank % 8`:
-    `iters` time-refinement steps + the final solve, one tgms_refine_loop_device call
-    (planned once)."""
+C5_PMC_FILE = "profiles/c5_pmc.json"
+
+
+def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_T=1.0, eta=0.1, reps=5):
+    """Config 5: a 1,048,576-trajectory ragged batch (M ~ U{2..16}) split over 8 GPUs
+    (the configuration's count, whatever N is) into contiguous cost-balanced shards
+    (shard.ragged_bounds); this rank solves shard `rank % 8`: `iters` time-refinement
+    steps + the final solve, one tgms_refine_loop_device call (planned once).
+    `ms_per_batch` is the median of HIP-event pairs around single calls on the launch
+    stream (the times are reset from a device copy before each call, outside the
+    events); the wall clock per call (host planning included) is beside it.
+
+    Roofline: the loop is FP64-VALU-bound.  `achieved` = the executed FP64 flops of one
+    call (committed PMC, profiles/c5_pmc.json) / the live event time, against the FP64
+    vector peak; the algorithmic HBM bytes (waypoints + times read, times + coefficients
+    + costs + statuses written) and their rate are beside it."""
     import torch
     from trajectory_generator_ros2_amd import shard as SH
     from trajectory_generator_ros2_amd import synthetic as S
@@ -167,29 +177,64 @@ def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_
     so, W, T, _ = SH.shard_csr(so_all, W_all, T_all, None, int(bounds[part]), int(bounds[part + 1]))
     del so_all, W_all, T_all
     B = len(so) - 1
+    Sg = int(so[-1])
     d_so = torch.from_numpy(so.astype(np.int32)).to(dev)
     dW = torch.from_numpy(W.reshape(-1, 3)).to(dev)
     T0 = torch.from_numpy(T.reshape(-1)).to(dev)
     dT = torch.empty_like(T0)
-    dC = torch.empty((int(so[-1]), 3, 8), dtype=torch.float64, device=dev)
+    dC = torch.empty((Sg, 3, 8), dtype=torch.float64, device=dev)
     dcost = torch.empty(B, dtype=torch.float64, device=dev)
+    dst = torch.empty(B, dtype=torch.int32, device=dev)
     sp = stream.cuda_stream
 
-    def run():
-        dT.copy_(T0)
-        solver.refine_loop_device(so, d_so, dW, dT, k_T, eta, iters, dC, dcost, stream=sp)
+    def call():
+        solver.refine_loop_device(so, d_so, dW, dT, k_T, eta, iters, dC, dcost, dst, stream=sp)
 
-    run()
+    for _ in range(2):
+        dT.copy_(T0)
+        call()
     torch.cuda.synchronize()
+    evs = []
+    for _ in range(reps):
+        dT.copy_(T0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        call()
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)[reps // 2]
     t0 = time.perf_counter()
     for _ in range(reps):
-        run()
+        dT.copy_(T0)
+        call()
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / reps * 1e3
-    return {"workload": f"config5: shard {part} of 8 (cost-balanced, {B} trajectories) of a {B_total}-trajectory "
+    wall = (time.perf_counter() - t0) / reps * 1e3
+    assert int((dst != 0).sum().item()) == 0, "refinement reported failures"
+    nbytes = (Sg + B) * 24 + 2 * Sg * 8 + Sg * 192 + B * (8 + 4) + (B + 1) * 4
+    line = {"workload": f"config5: shard {part} of 8 (cost-balanced, {B} trajectories) of a {B_total}-trajectory "
                         f"ragged batch, M~U{{2..16}}, {iters} refinement steps + final solve",
-            "ms_per_batch": ms, "trajectories_per_s": B / (ms * 1e-3), "segments": int(so[-1]),
-            "k_T": k_T, "eta": eta}
+            "ms_per_batch": ms, "ms_wall_per_call": wall, "trajectories_per_s": B / (ms * 1e-3), "segments": Sg,
+            "k_T": k_T, "eta": eta,
+            "timing": "median of single-call HIP event pairs on the launch stream; wall per call beside"}
+    try:
+        pmc = json.load(open(os.path.join(ROOT, C5_PMC_FILE)))["c5_share"]
+    except (OSError, ValueError, KeyError):
+        pmc = None
+    hbm = {"algorithmic_bytes_per_call": nbytes, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
+           "frac_of_peak": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "traffic": pmc["hbm_bytes_per_call"] if pmc else None}
+    if pmc:
+        tf = pmc["fp64_flops_per_call"] / (ms * 1e-3) / 1e12
+        line["roofline"] = {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                            "frac": tf / FP64_PEAK_TFS, "flops_per_call": pmc["fp64_flops_per_call"],
+                            "flops_source": f"{C5_PMC_FILE} (executed FP64 flops, rocprofv3 --pmc of "
+                                            f"scripts/c5bench.py: the same call), / this run's event time",
+                            "valu_issue_frac": pmc["valu_insts_per_call"] * 4 / (1024 * 2.4e9 * ms * 1e-3),
+                            "hbm": hbm, "kernels": "k_refine_loop_multi<1,11> + <12,16>, concurrent"}
+    else:
+        line["roofline"] = {"bound": "fp64_valu", "achieved": None, "hbm": hbm}
+    return line
 
 
 def config4_line(solver, M, dev, stream, world, rank, B=131072, chunks=8, reps=3):

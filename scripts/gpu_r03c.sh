@@ -11,5 +11,7 @@ echo "pytest exit $c"; tail -3 $OUT/pytest_c.log
 timeout -k 10 300 python3 scripts/c4full.py > $OUT/c4full_c.json 2> $OUT/c4full_c.err; c=$?
 echo "c4 exit $c"; cat $OUT/c4full_c.json; [ $c -eq 0 ] || exit $c
 timeout -k 10 300 python3 scripts/c5bench.py > $OUT/c5bench_c.json 2> $OUT/c5bench_c.err; c=$?
-echo "c5 exit $c"; cat $OUT/c5bench_c.json
+echo "c5 exit $c"; cat $OUT/c5bench_c.json; [ $c -eq 0 ] || exit $c
+timeout -k 10 300 python3 scripts/bandbench.py > $OUT/band_c.json 2> $OUT/band_c.err; c=$?
+echo "band exit $c"; cat $OUT/band_c.json
 exit $c

@@ -37,6 +37,10 @@ namespace {
 // Waves per SIMD the register allocation must allow: two for the axis-sequential
 // solve while its state fits 256 registers without spilling (M <= 11), else one.
 #define TGMS_WAVES(M) ((M) <= TGMS_TWO_WAVE_MAX_M ? 2 : 1)
+// One-wave-per-SIMD kernels solve the three axes side by side (pair_solve_joint).
+#ifndef TGMS_JOINT_AXES
+#define TGMS_JOINT_AXES 1
+#endif
 
 // Scheduling fence between unrolled chain / emission steps.  The compiler-level
 // memory clobber also stops CSE of LDS reads across steps: re-reading LDS is far
@@ -81,8 +85,8 @@ constexpr int OSTRIDE = 10;
 template <int M>
 struct In {
     double W[(M + 1) * 3 * PSTRIDE];
-    double T[M * PSTRIDE];
-    double R[M * PSTRIDE];  // 1/T, computed once while staging
+    double R[M * PSTRIDE];  // 1/T, computed once while staging (T itself is not staged:
+                            // at 2.9 KB for M = 11 it cost the 2-wave kernels their 8th wave per CU)
     int64_t base[TPW];      // coefficient offset (doubles) of each slot's trajectory
     int bad[TPW];
 };
@@ -102,13 +106,11 @@ static_assert(OSTRIDE % 2 == 0, "staged rows must keep 16-B alignment");
 // knot M-j, virtual segment i = physical segment M-1-i).
 struct LaneView {
     const double* Wb;  // &W[phys knot of virtual knot 0][axis 0][slot]
-    const double* Tb;  // &T[phys segment of virtual segment 0][slot] (transposed layout only)
     const double* Rb;  // &R[...]
     int kstep;         // +-3 fields per virtual knot (x the field stride)
     int sstep;         // +-1 segment per virtual segment (x the field stride)
     int astep;         // doubles between the axes of one knot: PSTRIDE (transposed) or 1 (raw)
     __device__ __forceinline__ double w(int j, int a) const { return Wb[j * kstep + a * astep]; }
-    __device__ __forceinline__ double t(int i) const { return Tb[i * sstep]; }
     __device__ __forceinline__ double r(int i) const { return Rb[i * sstep]; }
 };
 
@@ -116,7 +118,6 @@ template <int M>
 __device__ __forceinline__ LaneView make_view(const In<M>& sm, int slot, bool right) {
     LaneView L;
     L.Wb = sm.W + (right ? M * 3 * PSTRIDE : 0) + slot;
-    L.Tb = sm.T + (right ? (M - 1) * PSTRIDE : 0) + slot;
     L.Rb = sm.R + (right ? (M - 1) * PSTRIDE : 0) + slot;
     L.kstep = right ? -3 * PSTRIDE : 3 * PSTRIDE;
     L.sstep = right ? -PSTRIDE : PSTRIDE;
@@ -146,7 +147,6 @@ template <int M>
 __device__ __forceinline__ LaneView make_view_raw(const RawIn<M>& sm, int slot, bool right) {
     LaneView L;
     L.Wb = sm.W + slot * RawIn<M>::NW + (right ? M * 3 : 0);
-    L.Tb = nullptr;
     L.Rb = sm.R + slot * M + (right ? M - 1 : 0);
     L.kstep = right ? -3 : 3;
     L.sstep = right ? -1 : 1;
@@ -598,6 +598,10 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
         o.J[e] += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
+        // anchored here: nothing stores these sums until the step's update, so without
+        // the anchor the compiler sinks every segment's cost arithmetic (and keeps all
+        // knot data live for it) to the end of the solve
+        asm volatile("" : "+v"(o.J[e]), "+v"(o.dJ[e]));
     } else {
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
@@ -759,6 +763,176 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     return TGMS_OK;
 }
 
+// Anchor a value at this point of the instruction stream: it must be computed before
+// the (volatile, ordered) statement, so IR-level sinking cannot pile every step's
+// arithmetic into one block after the last scheduling fence (which only orders the
+// machine scheduler).
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin33(double (&m)[3][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) pin(m[i][j]);
+}
+
+// The same solve with the three axes side by side in every knot step (knot-major
+// instead of axis-major), for the kernels that run at one wave per SIMD anyway
+// (M > TGMS_TWO_WAVE_MAX_M): the per-knot couplings and powers are formed once
+// instead of once per axis, and the three substitution chains are independent work
+// for the scheduler (one wave per SIMD has no second wave to hide their latency).
+// It keeps three axes' knot data live (+54 doubles); that only fits the one-wave
+// budget.  Per axis the same operations in the same order as pair_solve_ax, and every
+// per-segment accumulation (GradAcc) still adds the axes in order 0, 1, 2: the results
+// are bit-identical.
+template <int M, bool HAS_ED, class Out, class V>
+__device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool right, V&& valid_src,
+                                                    const double* __restrict__ ed, const Out& O) {
+    using CH = Chain<M>;
+    constexpr int nL = CH::nL, nR = CH::nR, NS = CH::NS, NE = CH::NE;
+    const int nl = right ? nR : nL;
+    const double sg = right ? -1.0 : 1.0;
+    AxFactors<M> Fa;
+    ax_factor<M>(Fa, L, right);
+    const bool spd_pair = Fa.spd && (pair_swap(Fa.spd ? 1.0 : 0.0) != 0.0);
+    const bool valid = get_valid(valid_src);
+    double fin = 0.0;
+    double u0[3][3];  // [axis][derivative], virtual-frame start derivatives
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
+            const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
+            u0[a][d] = right ? ((d == 1) ? s1 : -s1) : s0;
+        }
+    // ---- forward substitution, three axes per knot ----
+    double Y[NS + 1][3][3];  // [knot][axis][derivative]
+    {
+        double pp[8];
+        rpowers(L.r(0), pp);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            SCHED_FENCE();
+            const int k = s + 1;
+            double pn[8];
+            rpowers(L.r(k), pn);
+            double B[3][3];
+            if (s >= 1) coupling(pp, B);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double y[3];
+                knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0[a], y);
+                if (s >= 1) {
+                    double v0, v1, v2;
+                    ldl3_solve(Fa.F[s - 1], Y[s - 1][a][0], Y[s - 1][a][1], Y[s - 1][a][2], v0, v1, v2);
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
+                }
+#pragma unroll
+                for (int d = 0; d < 3; ++d) Y[s][a][d] = y[d];
+            }
+            pin33(Y[s]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+        }
+    }
+    SCHED_FENCE();
+    // ---- interface, per axis (bit-identical on both lanes) ----
+    double xm[3][3];
+    {
+        double Cc[3][3];
+        {
+            double pc[8];
+            rpowers(L.r(nl), pc);
+            coupling(pc, Cc);
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double yL[3], yR[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const double yv = (nR > nL) ? (right ? Y[NS - 1][a][d] : Y[nL - 1][a][d]) : Y[nL - 1][a][d];
+                const double yp = (d == 1) ? yv : sg * yv;
+                yL[d] = pair_even(yp);
+                yR[d] = pair_odd(yp);
+            }
+            double g0, g1, g2;
+            ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) yL[d] -= Cc[d][0] * g0 + Cc[d][1] * g1 + Cc[d][2] * g2;
+            double xc0, xc1, xc2, x10, x11, x12;
+            ldl3_solve(Fa.FS, yL[0], yL[1], yL[2], xc0, xc1, xc2);
+            const double b0 = yR[0] - (Cc[0][0] * xc0 + Cc[1][0] * xc1 + Cc[2][0] * xc2);
+            const double b1 = yR[1] - (Cc[0][1] * xc0 + Cc[1][1] * xc1 + Cc[2][1] * xc2);
+            const double b2 = yR[2] - (Cc[0][2] * xc0 + Cc[1][2] * xc1 + Cc[2][2] * xc2);
+            ldl3_solve(Fa.FR, b0, b1, b2, x10, x11, x12);
+            xm[a][0] = right ? -x10 : xc0;
+            xm[a][1] = right ? x11 : xc1;
+            xm[a][2] = right ? -x12 : xc2;
+            const double o0 = right ? -xc0 : x10, o1 = right ? xc1 : x11, o2 = right ? -xc2 : x12;
+            if (nR > nL) {
+                Y[nL][a][0] = right ? Y[nL][a][0] : o0;
+                Y[nL][a][1] = right ? Y[nL][a][1] : o1;
+                Y[nL][a][2] = right ? Y[nL][a][2] : o2;
+                Y[nR][a][0] = right ? o0 : Y[nR][a][0];
+                Y[nR][a][1] = right ? o1 : Y[nR][a][1];
+                Y[nR][a][2] = right ? o2 : Y[nR][a][2];
+            } else {
+                Y[nL][a][0] = o0;
+                Y[nL][a][1] = o1;
+                Y[nL][a][2] = o2;
+            }
+            fin += (xc0 + xc1) + (xc2 + x10) + (x11 + x12);
+        }
+    }
+    // ---- back substitution, three axes per knot; segment s+1 emitted right after ----
+#pragma unroll
+    for (int s = NS - 1; s >= 0; --s) {
+        SCHED_FENCE();
+        const bool at_end = (s == nl - 1);
+        const bool inside = (s < nl - 1);
+        if (s + 1 < NS) {
+            double B[3][3];
+            {
+                double pb[8];
+                rpowers(L.r(s + 1), pb);
+                coupling(pb, B);
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double b[3], x0, x1, x2;
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+                    b[d] = Y[s][a][d] - (B[d][0] * Y[s + 1][a][0] + B[d][1] * Y[s + 1][a][1] + B[d][2] * Y[s + 1][a][2]);
+                ldl3_solve(Fa.F[s], b[0], b[1], b[2], x0, x1, x2);
+                Y[s][a][0] = at_end ? xm[a][0] : (inside ? x0 : Y[s][a][0]);
+                Y[s][a][1] = at_end ? xm[a][1] : (inside ? x1 : Y[s][a][1]);
+                Y[s][a][2] = at_end ? xm[a][2] : (inside ? x2 : Y[s][a][2]);
+                fin += inside ? (x0 + x1) + x2 : 0.0;
+            }
+            pin33(Y[s]);
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int d = 0; d < 3; ++d) Y[s][a][d] = at_end ? xm[a][d] : Y[s][a][d];
+        }
+        if (s + 1 < NE) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+                emit_axis<M, Out>(O, L, right, s + 1, a, Y[s][a], Y[s + 1][a], s + 1 < nR, !spd_pair);
+        }
+    }
+    SCHED_FENCE();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) emit_axis<M, Out>(O, L, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+    const double fin_pair = fin + pair_swap(fin);
+    if (!valid) return TGMS_ERR_INVALID_ARG;
+    if (!spd_pair) return TGMS_ERR_SINGULAR;
+    if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
+    return TGMS_OK;
+}
+
 // Emit one segment (virtual knots 0, 1 with derivatives xs, xe [derivative][axis]).
 template <int M, class Out>
 __device__ __forceinline__ void emit_all_axes(const Out& O, const LaneView& L, bool right,
@@ -826,7 +1000,10 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
         if (!finite(fin_pair)) return TGMS_ERR_NONFINITE;
         return TGMS_OK;
     } else {
-        return pair_solve_ax<M, HAS_ED, Out>(L, right, valid_src, ed, O);
+        if constexpr (M > TGMS_TWO_WAVE_MAX_M && TGMS_JOINT_AXES)
+            return pair_solve_joint<M, HAS_ED, Out>(L, right, valid_src, ed, O);
+        else
+            return pair_solve_ax<M, HAS_ED, Out>(L, right, valid_src, ed, O);
     }
 }
 
@@ -840,7 +1017,6 @@ __device__ __forceinline__ void stage_row_w(In<M>& sm, int t, int q, double v) {
 }
 template <int M>
 __device__ __forceinline__ void stage_row_t(In<M>& sm, int t, int q, double v) {
-    sm.T[q * PSTRIDE + t] = v;
     sm.R[q * PSTRIDE + t] = fast_rcp(v);
     if (!finite_pos(v)) atomicOr(&sm.bad[t], 1);
 }
@@ -851,10 +1027,7 @@ template <int M>
 __device__ __forceinline__ void sanitize(In<M>& sm, int lane) {
     if (lane < TPW && sm.bad[lane]) {
         for (int q = 0; q < (M + 1) * 3; ++q) sm.W[q * PSTRIDE + lane] = 0.0;
-        for (int q = 0; q < M; ++q) {
-            sm.T[q * PSTRIDE + lane] = 1.0;
-            sm.R[q * PSTRIDE + lane] = 1.0;
-        }
+        for (int q = 0; q < M; ++q) sm.R[q * PSTRIDE + lane] = 1.0;
     }
 }
 
@@ -1207,9 +1380,12 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
     }
     // this lane updates the times of its half of the segments; between steps they live
-    // in the stage only (an invalid trajectory keeps its times: its stage row was
-    // sanitised, so the cost reads them from memory, and nothing is written back)
+    // in its registers (and as 1/T in the stage); an invalid trajectory keeps its times
+    // (its stage row was sanitised to unit times; nothing is written back)
     const int nmine = right ? CH::nR : NE;
+    double Tl[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) Tl[e] = (live && e < nmine) ? T[s0 + (right ? M - 1 - e : e)] : 0.0;
     __syncthreads();
     sanitize(sm.in, lane);
     __syncthreads();
@@ -1226,11 +1402,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         double Fl = 0.0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
-            if (live && e < nmine) {
-                const int phys = right ? M - 1 - e : e;
-                const double tl = valid ? sm.in.T[phys * PSTRIDE + slot] : T[s0 + phys];
-                Fl += G.J[e] + kT * tl;
-            }
+            if (live && e < nmine) Fl += G.J[e] + kT * Tl[e];
         }
         const double F = Fl + pair_swap(Fl);
         if (it == iters) {
@@ -1243,11 +1415,11 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         for (int e = 0; e < NE; ++e) {
             if (live && valid && e < nmine) {
                 const int phys = right ? M - 1 - e : e;
-                const double tl = sm.in.T[phys * PSTRIDE + slot];
+                const double tl = Tl[e];
                 double dtau = -eta * tl * (G.dJ[e] + kT) / F;
                 dtau = fmin(fmax(dtau, -0.5), 0.5);
                 const double tn = ok ? tl * exp(dtau) : tl;
-                sm.in.T[phys * PSTRIDE + slot] = tn;
+                Tl[e] = tn;
                 sm.in.R[phys * PSTRIDE + slot] = fast_rcp(tn);
             }
         }
@@ -1255,10 +1427,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
     }
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-        if (live && valid && e < nmine) {
-            const int phys = right ? M - 1 - e : e;
-            T[s0 + phys] = sm.in.T[phys * PSTRIDE + slot];
-        }
+        if (live && valid && e < nmine) T[s0 + (right ? M - 1 - e : e)] = Tl[e];
     }
     if (C) {
         __syncthreads();
@@ -1421,13 +1590,6 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(Group
 // the (volatile, ordered) statement, so IR-level sinking cannot pile every knot's
 // arithmetic into one block after the last scheduling fence (which only orders the
 // machine scheduler): without the anchors the kernel needs > 700 registers.
-__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ void pin33(double (&m)[3][3]) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) pin(m[i][j]);
-}
 __device__ __forceinline__ void pin_ldl3(Ldl3& f) {
     pin(f.i0);
     pin(f.i1);
