@@ -433,12 +433,15 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         tgms::GroupTable tab[2];
         class_tables(p, tab);
         std::vector<std::function<hipError_t(hipStream_t)>> jobs;
-        for (int k = 1; k >= 0; --k)
+        static const bool two_wave_first = std::getenv("TGMS_LOOP_CLASS_A_FIRST") != nullptr;
+        for (int i = 0; i < 2; ++i) {
+            const int k = two_wave_first ? i : 1 - i;
             if (tab[k].ngroups)
                 jobs.push_back([&, k](hipStream_t q) {
                     return tgms::launch_refine_loop_multi(k, tab[k], d_so, W, T[0], ED, kT, eta, iters, cost, C, st,
                                                           q);
                 });
+        }
         tgms_status s = run_parallel(h, stream, jobs);
         if (s != TGMS_OK) return s;
         *cur = 0;
@@ -564,6 +567,10 @@ void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* b
     bounds[0] = 0;
     if (B == 0) {
         for (int k = 1; k <= parts; ++k) bounds[k] = 0;
+        return;
+    }
+    if (parts == 1) {
+        bounds[1] = B;
         return;
     }
     if (uniform_m > 0) {
