@@ -666,6 +666,23 @@ def config5_full_line(devs, reps=3, B_total=1048576, iters=10, k_T=1.0, eta=0.1)
             "status_failures": bad, "costs_finite": finite}
 
 
+def full_lines_child(n: int, timeout_s: float) -> dict:
+    """config4_full / config5_full over devices 0..n-1, run by `bench.py --gpus n
+    --full-lines-only` as a child process (started fresh, not forked from this GPU
+    process's state) under `timeout_s`; its JSON, or an error record."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(n), "--full-lines-only", "--cpu-seconds", "0"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"the {n}-device library side lines exceeded {timeout_s:.0f} s and were abandoned"}
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"child exited {r.returncode}: {r.stderr.strip()[-400:]}"}
+    return json.loads(lines[-1])
+
+
 def _side(name, fn):
     """A side line that fails reports its error instead of ending the run."""
     try:
@@ -707,6 +724,11 @@ def main():
     ap.add_argument("--node-line", type=int, default=1, help="config-1 node-path latency side line: 1/0")
     ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
+    ap.add_argument("--full-lines-only", action="store_true",
+                    help="internal: print only the config4_full / config5_full lines over devices 0..N-1 (the "
+                         "parent runs them in this child process at N > 1, under a time limit)")
+    ap.add_argument("--full-lines-timeout", type=float, default=300.0,
+                    help="seconds the N > 1 library multi-GPU side lines may take before they are abandoned")
     args = ap.parse_args()
 
     import torch
@@ -729,6 +751,14 @@ def main():
     torch.cuda.set_device(devs[0])
 
     from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
+
+    if args.full_lines_only:
+        from trajectory_generator_ros2_amd.solver import Solver
+        with Solver(devs[0]) as ref:
+            out = {"config4_full": _side("config4_full", lambda: config4_full_line(devs, ref)),
+                   "config5_full": _side("config5_full", lambda: config5_full_line(devs))}
+        print(json.dumps(out), flush=True)
+        return
 
     B, M, sets = args.batch, args.segments, max(1, args.sets)
     method = METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED
@@ -866,17 +896,30 @@ def main():
         solver.set_method(METHOD_REDUCED)
         del dC3
 
+    # N > 1 (or TGMS_BENCH_FULL_CHILD=1, to rehearse it on one GPU): the full-size lines
+    # run in a child process
+    child_full = len(devs) > 1 or os.environ.get("TGMS_BENCH_FULL_CHILD") == "1"
     config5 = config5_full = None
     if args.config5 and M == 10:
         config5 = config5_line(solver, dev, stream, world, rank)
-        if world == 1:
+        if world == 1 and len(devs) == 1 and not child_full:
             config5_full = _side("config5_full", lambda: config5_full_line(devs))
 
     config4 = config4_full = None
     if args.config4 and M == 10:
         config4 = config4_line(solver, M, dev, stream, world, rank)
-        if world == 1:
+        if world == 1 and len(devs) == 1 and not child_full:
             config4_full = _side("config4_full", lambda: config4_full_line(devs, solver))
+
+    if world == 1 and child_full and (args.config4 or args.config5) and M == 10:
+        # the library's own multi-GPU path (one RCCL communicator per device inside this
+        # process's library handle) runs in a child process under a time limit: a stuck
+        # collective then costs this side line, never the headline
+        full = full_lines_child(len(devs), args.full_lines_timeout)
+        if args.config4:
+            config4_full = full.get("config4_full", full)
+        if args.config5:
+            config5_full = full.get("config5_full", full)
 
     sampler = None
     if args.sample_traj > 0:
