@@ -65,15 +65,16 @@ __device__ __forceinline__ double dfac(int j, int k) {
 
 // Entries of the interleaved KKT, framed in the block of segment i: offsets 0..7 are
 // c_i, 8..13 the rows of the knot after segment i (the end rows if i = M-1), -4..-1 the
-// start rows (i = 0).  Every entry is coef * V_i[idx] with V_i = [1, T_i^0..T_i^7,
-// 2Q_i (16)] staged per trajectory in LDS, and (coef, idx) depends only on the block
-// variant (first / last segment), the row offset o and the diagonal offset d = c - r, so
-// the pattern is a small table built once per wavefront: an entering row costs two LDS
-// reads per lane instead of a divergent case analysis.  Same entries as oracle
-// assemble_kkt_cont; tests/test_oracle.py pins the band.
-constexpr int VAL = 25;               // V_i stride
+// start rows (i = 0).  Every entry is coef * V_i[idx] with V_i = [1, T_i^0..T_i^7]
+// staged per trajectory in LDS, or (idx = 9 + e) a 2Q_i entry 2 (coef T_i^e / e), formed
+// in the order the oracle assembles it (q = dfac dfac T^e / e, K = 2 q); (coef, idx)
+// depends only on the block variant (first / last segment), the row offset o and the
+// diagonal offset d = c - r, so the pattern is a small table built once per workgroup:
+// an entering row costs two LDS reads per lane instead of a divergent case analysis.
+// Same entries as oracle assemble_kkt_cont; tests/test_oracle.py
+// pins the band.
+constexpr int VAL = 9;                // V_i stride: [1, T_i^0..T_i^7]
 constexpr int NOFF = 18;              // row offsets -4..13
-constexpr int NDESC = 4 * NOFF * WC;  // variants x offsets x diagonals
 
 __host__ __device__ constexpr int pack(int coef, int idx) { return coef * 32 + idx; }
 
@@ -93,7 +94,8 @@ __device__ int desc_entry(int vv, int o, int d) {
     }
     if (o < 8) {  // stationarity row of coefficient j of segment i
         const int j = o;
-        if (oc >= 0 && oc < 8) return (j >= 4 && oc >= 4) ? pack(1, 9 + (j - 4) * 4 + (oc - 4)) : 0;
+        if (oc >= 0 && oc < 8)  // 2Q_i: idx 9 + e stands for 2 (coef T_i^e / e), e = j + k - 7
+            return (j >= 4 && oc >= 4) ? pack((int)(dfac(j, 4) * dfac(oc, 4)), 9 + (j + oc - 7)) : 0;
         if (oc >= 14) return 0;
         if (oc >= 8) {
             const int t = oc - 8;
@@ -113,43 +115,6 @@ __device__ int desc_entry(int vv, int o, int d) {
     return 0;
 }
 
-// Row r (wave-uniform) at this lane's column c; lanes WC..WC+2 return the right-hand
-// side b_r of axis hl - WC.  Branch-free in the lane: every lane reads its matrix entry
-// and the right-hand-side candidate and selects (a divergent split costs more issue
-// slots than the two extra LDS reads).
-template <int M, bool HAS_ED>
-__device__ __forceinline__ double row_entry(int hl, int r, int c, const int* desc, const double* val,
-                                            const double* w, const double* ed) {
-    constexpr int N = 14 * M + 2;
-    if (r >= N) return 0.0;
-    const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
-    const int o = r - (4 + 14 * i);
-    // right-hand-side source (uniform): waypoint row wr or end-derivative base eb
-    int wr = -1, eb = -1;
-    if (o < 0) {
-        if (o == -4) wr = 0;
-        else eb = (o + 3) * 3;
-    } else if (o >= 8) {
-        const int t = o - 8;
-        if (i == M - 1) {
-            if (t == 0) wr = M;
-            else eb = 9 + (t - 1) * 3;
-        } else if (t <= 1) {
-            wr = i + 1;
-        }
-    }
-    const int ax = min(max(hl - WC, 0), 2);
-    const double rw = w[max(wr, 0) * 3 + ax];
-    const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
-    const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
-    const int d = c - r;
-    const bool inb = (c < N) && d >= -KL && d <= KL;
-    const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
-    const int de = desc[(vv * NOFF + o + 4) * WC + min(max(d, -KL), KL) + KL];
-    const double m = (double)(de >> 5) * val[i * VAL + (de & 31)];
-    return (hl < WC) ? (inb ? m : 0.0) : ((hl < WC + 3) ? rhs : 0.0);
-}
-
 // 1/x: hardware reciprocal + two Newton steps (within an ulp; the pivots only scale)
 __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
@@ -158,23 +123,28 @@ __device__ __forceinline__ double recip(double x) {
 }
 
 // ---------------------------------------------------------------------------
-// Row-lane mapping: a 16-lane DPP row per trajectory, four trajectories per wavefront.
-// Lane j < WR holds one window row: its entries at columns k..k+18 in registers
-// u[c mod 19] (static register names under a 19-step unroll) and its 3 right-hand
-// sides.  Rows never move between lanes: the pivot search is a DPP max over the row's
-// lanes (ties to the lowest position in the permuted order, as LAPACK and the oracle),
-// the interchange is a swap of two position labels, and the pivot row reaches the other
-// lanes through one LDS broadcast.  The pivot lane leaves with its row (it becomes U row
-// k in the slab) and takes the entering row k+10, which the group assembles
-// column-parallel (two entries per lane) and hands over through LDS.  A step issues
-// ~160 VALU + ~100 SALU instructions per wavefront for four trajectories (the
-// column-lane mapping: ~105 VALU + ~40 SALU for two).
-constexpr int QG = 16;                  // lanes per trajectory (one DPP row)
-constexpr int QT = W64 / QG;            // trajectories per wavefront
+// Octet mapping (round 3): eight lanes per trajectory in the forward elimination, eight
+// trajectories per wavefront.  Lane j < 5 holds TWO window rows, 2j and 2j+1: their
+// entries at columns k..k+18 in registers u[c mod 19] (static names under a 19-step
+// unroll) and their 3 right-hand sides.  Rows never move between lanes: the pivot search
+// is a DPP max over the octet (quad swaps and the half-row mirror), then the lowest
+// position among the maxima (ties to the lowest position in the permuted order, as
+// LAPACK and the oracle), the interchange swaps two position labels, and the pivot row
+// reaches the other lanes through one LDS broadcast that each lane reads once for both
+// of its rows.  The per-step work that does not grow with the rows -- pivot search,
+// pivot-row hand-over, entering row, bookkeeping -- is paid once per eight trajectories
+// (round 2's row-lane mapping: once per four, a 16-lane row per trajectory with one
+// window row per lane).  Back substitution keeps the 16-lane rows (four trajectories at
+// a time, two passes).
+constexpr int QG = 16;                  // back substitution: lanes per trajectory (one DPP row)
+constexpr int QT = W64 / QG;            // back substitution: trajectories per pass
+constexpr int OG = 8;                   // forward elimination: lanes per trajectory (half a DPP row)
+constexpr int OT = W64 / OG;            // trajectories per wavefront
+constexpr int OL = WR / 2;              // lanes holding window rows (two each)
 constexpr int QW = 4;                   // wavefronts per workgroup (share the entry table)
 constexpr int QS = UW + 2;              // LDS row stride of the pivot / entering rows (16-B aligned)
 #ifndef TGMS_BAND_WAVES_PER_EU
-#define TGMS_BAND_WAVES_PER_EU 2           // register budget: 256 VGPRs, no spills in the step loops
+#define TGMS_BAND_WAVES_PER_EU 2
 #endif
 
 using gdouble = __attribute__((address_space(1))) double;  // global: keeps slab accesses off the flat path
@@ -182,15 +152,6 @@ using gdouble = __attribute__((address_space(1))) double;  // global: keeps slab
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-}
-
-// Column held by register t at step k (R = k mod WC): the c = t (mod WC) in [k+1, k+WC]
-// once column k has left (the entering row's columns).
-template <int R>
-__device__ __forceinline__ int enter_col(int k, int t) {
-    int d = t - (R + 1) % WC;
-    d += (d < 0) ? WC : 0;
-    return k + 1 + d;
 }
 
 // Lane-dependent values re-derived inside every unrolled step: an opaque copy keeps
@@ -205,25 +166,37 @@ __device__ __forceinline__ gdouble* opaque(gdouble* p) {
     return p;
 }
 
-// Entering row k+WR from its structural nonzeros (at most NE = 10 per row of the
-// interleaved KKT): lanes 0..10 zero the row's 22 slots, then lane j < NE writes
-// nonzero j of the row's pattern (coef * V_i[idx] at column r + d) and lanes NE..NE+2 the
-// right-hand sides.  The row's block, offset and right-hand-side source are wave-uniform
-// (scalar unit).  Same entries as row_entry (the list is built from the same table).
+// A row of the interleaved KKT from its structural nonzeros (at most NE = 10 per row):
+// a per-(block variant, row offset) list of (coefficient, diagonal offset, V index),
+// built once per workgroup from the entry table.
 constexpr int NE = 10;                  // structural nonzeros per row, at most
 constexpr int NPAT = 4 * NOFF;          // (variant, row offset) patterns
 
 __host__ __device__ constexpr int pack_ent(int coef, int d, int idx) { return (coef << 10) | ((d + KL) << 5) | idx; }
 
-template <int M, bool HAS_ED, int R>
-__device__ __forceinline__ void enter_row(int k, int j, const int* ents, const double* val, const double* w,
-                                          const double* ed, double* E) {
+// value of a packed entry of segment block vi (V_i = [1, T_i^0..T_i^7])
+__device__ __forceinline__ double ent_value(int e, const double* vi) {
+    const int idx = e & 31;
+    const double c = (double)(e >> 10);
+    if (idx < VAL) return c * vi[idx];
+    const int ex = idx - VAL;  // a 2Q_i entry: 2 (dfac dfac T^e / e), as the oracle forms it
+    return 2.0 * (c * vi[1 + ex] / (double)ex);
+}
+
+// Assemble row r (wave-uniform) into the octet's LDS row E in register-slot order:
+// column r + d goes to slot (base + d) mod 19 (base = r mod 19 when column c sits in
+// register c mod 19), the 3 right-hand sides to slots 19..21.  The octet's 8 lanes
+// zero the 22 slots (11 16-B writes), then lane j writes items j and j + 8 of the row's
+// 13 (10 nonzeros, 3 right-hand sides).  LDS operations of a wave execute in order, so
+// the zeros land before the items.
+template <int M, bool HAS_ED>
+__device__ __forceinline__ void assemble_row(int r, int base, int j, const int* ents, const double* val,
+                                             const double* w, const double* ed, double* E) {
     constexpr int N = 14 * M + 2;
-    const int r = k + WR;
     const bool live_r = r < N;
     const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
     const int o = live_r ? r - (4 + 14 * i) : 0;
-    int wr = -1, eb = -1;
+    int wr = -1, eb = -1;  // right-hand-side source (uniform): waypoint row, end-derivative base
     if (o < 0) {
         if (o == -4) wr = 0;
         else eb = (o + 3) * 3;
@@ -237,66 +210,102 @@ __device__ __forceinline__ void enter_row(int k, int j, const int* ents, const d
         }
     }
     const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
-    if (j < UW / 2) reinterpret_cast<double2*>(E)[j] = make_double2(0.0, 0.0);
-    const int e = ents[(vv * NOFF + o + 4) * NE + min(j, NE - 1)];
-    const int d = ((e >> 5) & 31) - KL;
-    const double v = (double)(e >> 10) * val[i * VAL + (e & 31)];
-    int t = R + WR + d;  // register slot of column r + d (in [k+1, k+19])
-    t -= (t >= WC) ? WC : 0;
-    const int ax = min(max(j - NE, 0), 2);
-    const double rw = w[max(wr, 0) * 3 + ax];
-    const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
-    const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
-    const bool put = live_r && ((j < NE) ? (e != 0) : (j < NE + 3));
-    if (put) E[(j < NE) ? t : WC + ax] = (j < NE) ? v : rhs;
+    double2* E2 = reinterpret_cast<double2*>(E);
+    E2[j] = make_double2(0.0, 0.0);
+    if (j < UW / 2 - OG) E2[OG + j] = make_double2(0.0, 0.0);
+    const int* list = ents + (vv * NOFF + o + 4) * NE;
+    const double* vi = val + i * VAL;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int n = j + OG * h;  // item n of 13
+        if (n < NE) {
+            const int e = list[n];
+            const int d = ((e >> 5) & 31) - KL;
+            int t = base + d;
+            t += (t < 0) ? WC : 0;
+            t -= (t >= WC) ? WC : 0;
+            if (live_r && e != 0) E[t] = ent_value(e, vi);
+        } else if (n < NE + 3) {
+            const int ax = n - NE;
+            const double rw = w[max(wr, 0) * 3 + ax];
+            const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
+            const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
+            if (live_r) E[WC + ax] = rhs;
+        }
+    }
+}
+
+// Take the assembled row from E into registers (11 16-B reads).
+__device__ __forceinline__ void take_row(const double* E, double (&u)[WC], double (&rh)[3]) {
+    const double2* E2 = reinterpret_cast<const double2*>(E);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        const double2 v = E2[q];
+        u[2 * q] = v.x;
+        u[2 * q + 1] = v.y;
+    }
+    const double2 v9 = E2[9], v10 = E2[10];
+    u[18] = v9.x;
+    rh[0] = v9.y;
+    rh[1] = v10.x;
+    rh[2] = v10.y;
+}
+
+// Hand a window row to the octet as U row k: [1/pivot, columns k+1..k+18, rhs].
+template <int R>
+__device__ __forceinline__ void put_pivot_row(double* P, double cv, const double (&u)[WC], const double (&rh)[3]) {
+    double2* P2 = reinterpret_cast<double2*>(P);
+    P2[0] = make_double2(recip(cv), u[(R + 1) % WC]);
+#pragma unroll
+    for (int q = 1; q < 9; ++q) P2[q] = make_double2(u[(R + 2 * q) % WC], u[(R + 2 * q + 1) % WC]);
+    P2[9] = make_double2(u[(R + 18) % WC], rh[0]);
+    P2[10] = make_double2(rh[1], rh[2]);
 }
 
 template <int M, bool HAS_ED, int R>
-__device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double (&rh)[3], int& pos, bool& sing,
-                                         double* P, double* E, gdouble* U, const int* ents, const double* val,
-                                         const double* w, const double* ed) {
+__device__ __forceinline__ void oct_step(int k, int j0, double (&u0)[WC], double (&u1)[WC], double (&r0)[3],
+                                         double (&r1)[3], int& pos0, int& pos1, bool& sing, double* P, double* E,
+                                         gdouble* U, const int* ents, const double* val, const double* w,
+                                         const double* ed) {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const int j = opaque(j0);
-    enter_row<M, HAS_ED, R>(k, j, ents, val, w, ed, E);
-    // pivot search in column k (register R) over the window lanes: DPP max of |a|, then
-    // the lowest position among the maxima
-    const double cv = u[R];
-    const bool win = j < WR;
-    double m = win ? fabs(cv) : -1.0;
+    assemble_row<M, HAS_ED>(k + WR, (R + WR) % WC, j, ents, val, w, ed, E);  // the entering row
+    // pivot search in column k (register R) over the octet's ten window rows
+    const bool win = j < OL;
+    const double c0 = u0[R], c1 = u1[R];
+    const double a0 = fabs(c0), a1 = fabs(c1);
+    double m = win ? fmax(a0, a1) : -1.0;
     m = fmax(m, dpp_f64<0xB1>(m));   // quad_perm [1,0,3,2]
     m = fmax(m, dpp_f64<0x4E>(m));   // quad_perm [2,3,0,1]
-    m = fmax(m, dpp_f64<0x141>(m));  // row_half_mirror
-    m = fmax(m, dpp_f64<0x140>(m));  // row_mirror
-    const bool eq = win && fabs(cv) == m;
-    int cp = eq ? pos : 0x7fffffff;
+    m = fmax(m, dpp_f64<0x141>(m));  // row_half_mirror: the octet
+    const bool eq0 = win && a0 == m, eq1 = win && a1 == m;
+    int cp = min(eq0 ? pos0 : 0x7fffffff, eq1 ? pos1 : 0x7fffffff);
     cp = min(cp, dpp_i32<0xB1>(cp));
     cp = min(cp, dpp_i32<0x4E>(cp));
     cp = min(cp, dpp_i32<0x141>(cp));
-    cp = min(cp, dpp_i32<0x140>(cp));
-    const bool piv = eq && pos == cp;
+    const bool piv0 = eq0 && pos0 == cp, piv1 = eq1 && pos1 == cp;
     sing = sing || !(m > 0.0);
-    // the pivot lane hands its row to the group through LDS ([1/pivot, columns
-    // k+1..k+18, rhs]: U row k), one 64-bit write per entry (no register shuffles)
-    if (piv) {
-        P[0] = recip(cv);
-#pragma unroll
-        for (int d = 1; d < WC; ++d) P[d] = u[(R + d) % WC];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) P[WC + a] = rh[a];
-    }
+    if (piv0) put_pivot_row<R>(P, c0, u0, r0);
+    if (piv1) put_pivot_row<R>(P, c1, u1, r1);
     __builtin_amdgcn_wave_barrier();
-    // U row k to the slab: lane j < 11 copies 16 B of it
-    if (j < UW / 2) {
-        const double2 v = reinterpret_cast<const double2*>(P)[j];
-        gdouble* Uk = U + (size_t)k * UW + 2 * j;
-        Uk[0] = v.x;
-        Uk[1] = v.y;
+    // U row k to the slab: 11 16-B pieces over the octet's 8 lanes
+    {
+        const double2* P2 = reinterpret_cast<const double2*>(P);
+        gdouble* Uk = U + (size_t)k * UW;
+        const double2 v = P2[j];
+        Uk[2 * j] = v.x;
+        Uk[2 * j + 1] = v.y;
+        if (j < UW / 2 - OG) {
+            const double2 v2 = P2[OG + j];
+            Uk[2 * (OG + j)] = v2.x;
+            Uk[2 * (OG + j) + 1] = v2.y;
+        }
     }
-    // rank-1 update of the other window rows (only they read the pivot row: the LDS
-    // pipe, not the VALU, is the tighter resource); column k leaves (register R becomes
+    // rank-1 update of both rows of every window lane (the pivot row with multiplier 0:
+    // it is replaced by the entering row below); column k leaves (register R becomes
     // column k+19, zero outside the entering row)
-    if (win && !piv) {
+    if (win) {
         double p[UW];
         const double2* Pd = reinterpret_cast<const double2*>(P);
 #pragma unroll
@@ -305,20 +314,30 @@ __device__ __forceinline__ void row_step(int k, int j0, double (&u)[WC], double 
             p[2 * q] = v.x;
             p[2 * q + 1] = v.y;
         }
-        const double l = cv * p[0];
+        const double l0 = piv0 ? 0.0 : c0 * p[0];
+        const double l1 = piv1 ? 0.0 : c1 * p[0];
 #pragma unroll
-        for (int d = 1; d < WC; ++d) u[(R + d) % WC] = fma(-l, p[d], u[(R + d) % WC]);
+        for (int d = 1; d < WC; ++d) {
+            u0[(R + d) % WC] = fma(-l0, p[d], u0[(R + d) % WC]);
+            u1[(R + d) % WC] = fma(-l1, p[d], u1[(R + d) % WC]);
+        }
 #pragma unroll
-        for (int a = 0; a < 3; ++a) rh[a] = fma(-l, p[WC + a], rh[a]);
+        for (int a = 0; a < 3; ++a) {
+            r0[a] = fma(-l0, p[WC + a], r0[a]);
+            r1[a] = fma(-l1, p[WC + a], r1[a]);
+        }
     }
-    u[R] = 0.0;
-    if (pos == k) pos = cp;  // interchange: the row at position k takes the pivot's position
-    if (piv) {               // the pivot lane takes row k+WR
-#pragma unroll
-        for (int t = 0; t < WC; ++t) u[t] = E[t];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) rh[a] = E[WC + a];
-        pos = k + WR;
+    u0[R] = 0.0;
+    u1[R] = 0.0;
+    if (pos0 == k) pos0 = cp;  // interchange: the row at position k takes the pivot's position
+    if (pos1 == k) pos1 = cp;
+    if (piv0) {  // the pivot's lane takes row k+WR into the pivot's slot
+        take_row(E, u0, r0);
+        pos0 = k + WR;
+    }
+    if (piv1) {
+        take_row(E, u1, r1);
+        pos1 = k + WR;
     }
     __builtin_amdgcn_wave_barrier();  // P and E are rewritten by the next step
 }
@@ -400,26 +419,19 @@ __device__ __forceinline__ void back_step(int k, int j0, int g, __amdgpu_buffer_
 }
 
 template <int M, bool HAS_ED>
-__global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_BAND_WAVES_PER_EU))) void k_band_kkt(int32_t n_traj, const int32_t* __restrict__ ids,
-                                                       const int32_t* __restrict__ seg_offsets,
-                                                       const double* __restrict__ W, const double* __restrict__ T,
-                                                       const double* __restrict__ ED, double* __restrict__ C,
-                                                       int32_t* __restrict__ status, double* __restrict__ scratch) {
+__global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_BAND_WAVES_PER_EU))) void k_band_kkt(
+    int32_t n_traj, const int32_t* __restrict__ ids, const int32_t* __restrict__ seg_offsets,
+    const double* __restrict__ W, const double* __restrict__ T, const double* __restrict__ ED, double* __restrict__ C,
+    int32_t* __restrict__ status, double* __restrict__ scratch) {
     constexpr int N = 14 * M + 2;
-    __shared__ int s_desc[NDESC];                            // entry pattern of the interleaved KKT
-    __shared__ int s_ents[NPAT * NE];                        // the same, as per-row nonzero lists
-    __shared__ double s_val[QW][QT][M * VAL];                // V_i = [1, T_i^0..T_i^7, 2Q_i] per segment
-    __shared__ double s_w[QW][QT][(M + 1) * 3];              // waypoints
-    __shared__ double s_ed[QW][QT][HAS_ED ? 18 : 1];         // end derivatives
-    __shared__ alignas(16) double s_piv[QW][QT][QS];         // pivot row of the current step
-    __shared__ alignas(16) double s_ent[QW][QT][QS];         // entering row of the current step
-    __shared__ double s_x[QW][QT][4];                        // back substitution: x_k broadcast
+    __shared__ int s_ents[NPAT * NE];                        // per-row nonzero lists of the interleaved KKT
+    __shared__ double s_val[QW][OT][M * VAL];                // V_i = [1, T_i^0..T_i^7] per segment
+    __shared__ double s_w[QW][OT][(M + 1) * 3];              // waypoints
+    __shared__ double s_ed[QW][OT][HAS_ED ? 18 : 1];         // end derivatives
+    __shared__ alignas(16) double s_piv[QW][OT][QS];         // pivot row of the current step
+    __shared__ alignas(16) double s_ent[QW][OT][QS];         // entering row of the current step
 
-    const int wv = threadIdx.x / W64, lane = threadIdx.x % W64, g = lane / QG;
-    for (int q = threadIdx.x; q < NDESC; q += QW * W64) {
-        const int vv = q / (NOFF * WC), rem = q - vv * NOFF * WC, o = rem / WC - 4, d = rem % WC - KL;
-        s_desc[q] = desc_entry(vv, o, d);
-    }
+    const int wv = threadIdx.x / W64, lane = threadIdx.x % W64, g = lane / OG;
     for (int q = threadIdx.x; q < NPAT; q += QW * W64) {
         const int vv = q / NOFF, o = q % NOFF - 4;
         int n = 0;
@@ -431,41 +443,40 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     }
     __syncthreads();
     const int wave_id = blockIdx.x * QW + wv;
-    gdouble* const U0 = (gdouble*)scratch + ((size_t)wave_id * QT + g) * (size_t)N * UW;
+    gdouble* const U0 = (gdouble*)scratch + ((size_t)wave_id * OT + g) * (size_t)N * UW;
     double* val = s_val[wv][g];
     double* w = s_w[wv][g];
     double* ed = s_ed[wv][g];
     double* P = s_piv[wv][g];
     double* E = s_ent[wv][g];
-    double* xs = s_x[wv][g];
-    const int nquads = (n_traj + QT - 1) / QT;
+    const int nocts = (n_traj + OT - 1) / OT;
 
-    for (int qd = wave_id; qd < nquads; qd += gridDim.x * QW) {
-        // per-quad opaque copies: the slab addresses must not be hoisted out of this loop
+    for (int oc = wave_id; oc < nocts; oc += gridDim.x * QW) {
+        // per-octet opaque copies: the slab addresses must not be hoisted out of this loop
         gdouble* const U = opaque(U0);
-        const int j = opaque(lane % QG);
-        const int bi = QT * qd + g;
+        const int j = opaque(lane % OG);
+        const int bi = OT * oc + g;
         const bool live = bi < n_traj;
-        const int32_t b = ids ? ids[live ? bi : QT * qd] : (live ? bi : QT * qd);
+        const int32_t b = ids ? ids[live ? bi : OT * oc] : (live ? bi : OT * oc);
         const int64_t s0 = seg_offsets ? (int64_t)seg_offsets[b] : (int64_t)b * M;
         const double* gw = W + (s0 + b) * 3;
         const double* gt = T + s0;
 
         // ---- stage inputs, validate (T > 0 finite; W, ED finite)
         bool ok = true;
-        for (int q = j; q < (M + 1) * 3; q += QG) {
+        for (int q = j; q < (M + 1) * 3; q += OG) {
             const double v = gw[q];
             w[q] = v;
             ok = ok && (v * 0.0 == 0.0);
         }
         if (HAS_ED) {
-            for (int q = j; q < 18; q += QG) {
+            for (int q = j; q < 18; q += OG) {
                 const double v = ED[(int64_t)b * 18 + q];
                 ed[q] = v;
                 ok = ok && (v * 0.0 == 0.0);
             }
         }
-        for (int i = j; i < M; i += QG) {
+        for (int i = j; i < M; i += OG) {
             const double t = gt[i];
             ok = ok && finite_pos(t);
             double p = 1.0;
@@ -477,70 +488,86 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
                 val[i * VAL + 1 + e] = p;
             }
         }
-        const unsigned long long badm = __ballot(!ok);
-        const bool valid = ((badm >> (QG * g)) & 0xffffull) == 0;
-        __builtin_amdgcn_wave_barrier();
-        for (int q = j; q < M * 16; q += QG) {
-            const int i = q >> 4, jj = 4 + ((q >> 2) & 3), kk = 4 + (q & 3), ex = jj + kk - 7;
-            val[i * VAL + 9 + (q & 15)] = 2.0 * (dfac(jj, 4) * dfac(kk, 4) * val[i * VAL + 1 + ex] / (double)ex);
-        }
+        const unsigned long long badm = __ballot(!ok);  // 8 bits per octet
         __builtin_amdgcn_wave_barrier();
 
-        // ---- forward elimination (a3): lane j < WR holds window row j
-        double u[WC], rh[3];
-        int pos = (j < WR) ? j : -1;  // position in the permuted order (-1: not a window lane)
+        // ---- the initial window: rows 0..9, assembled through E one at a time; lane
+        // j < 5 takes rows 2j (u0) and 2j+1 (u1)
+        double u0[WC], u1[WC], r0[3], r1[3];
 #pragma unroll
-        for (int t = 0; t < WC; ++t) u[t] = (j < WR) ? row_entry<M, HAS_ED>(t, j, t, s_desc, val, w, ed) : 0.0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) rh[a] = (j < WR) ? row_entry<M, HAS_ED>(WC + a, j, 0, s_desc, val, w, ed) : 0.0;
+        for (int rr = 0; rr < WR; ++rr) {
+            assemble_row<M, HAS_ED>(rr, rr, j, s_ents, val, w, ed, E);
+            __builtin_amdgcn_wave_barrier();
+            if (j == rr / 2) {
+                if (rr & 1)
+                    take_row(E, u1, r1);
+                else
+                    take_row(E, u0, r0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        int pos0 = (j < OL) ? 2 * j : -1, pos1 = (j < OL) ? 2 * j + 1 : -1;  // positions in the permuted order
         bool sing = false;
+
+        // ---- forward elimination (a3)
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) row_step<M, HAS_ED, R>(k0 + R, j, u, rh, pos, sing, P, E, U, s_ents, val, w, ed);
+    if (k0 + R < N) oct_step<M, HAS_ED, R>(k0 + R, j, u0, u1, r0, r1, pos0, pos1, sing, P, E, U, s_ents, val, w, ed);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
         }
         const unsigned long long singm = __ballot(sing);
-        const bool singular = ((singm >> (QG * g)) & 0xffffull) != 0;
-        const bool emit = live && valid && !singular;
 
-        // ---- back substitution.  The U rows this wave stored are read back by other lanes
-        // of the wave: wait for the stores to reach L2 and read them with L1-bypassing loads
-        // (the slab is reused by the next quad, so L1 may hold the previous one's lines)
+        // ---- back substitution, 16-lane rows, four trajectories per pass.  The U rows
+        // this wave stored are read back by other lanes of the wave: wait for the stores to
+        // reach L2 and read them with L1-bypassing loads (the slab is reused by the next
+        // octet, so L1 may hold the previous one's lines)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         constexpr int kN = N - 1;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            scratch + (size_t)wave_id * QT * N * UW, (short)0, QT * N * UW * 8, 0x00020000);
-        double2 ur[WC];
+            scratch + (size_t)wave_id * OT * N * UW, (short)0, OT * N * UW * 8, 0x00020000);
+        const int jq = opaque(lane % QG);
+#pragma unroll 1
+        for (int pass = 0; pass < OT / QT; ++pass) {
+            const int slot = pass * QT + lane / QG;  // trajectory slot of this 16-lane row
+            const int bq = OT * oc + slot;
+            const bool liveq = bq < n_traj;
+            const int32_t bb = ids ? ids[liveq ? bq : OT * oc] : (liveq ? bq : OT * oc);
+            const int64_t sq = seg_offsets ? (int64_t)seg_offsets[bb] : (int64_t)bb * M;
+            const bool valid = ((badm >> (OG * slot)) & 0xffull) == 0;
+            const bool singular = ((singm >> (OG * slot)) & 0xffull) != 0;
+            const bool emit = liveq && valid && !singular;
+            double2 ur[WC];
 #pragma unroll
-        for (int S = 0; S < WC; ++S) ur[S] = ld_row16(rs, row_off(g, j, kN - S, N));
-        double xa[3], xb[3];
+            for (int S = 0; S < WC; ++S) ur[S] = ld_row16(rs, row_off(slot, jq, kN - S, N));
+            double xa[3], xb[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            xa[a] = (j == 10) ? (a == 1 ? -1.0 : 0.0) : 0.0;
-            xb[a] = (j == 9) ? (a == 0 ? -1.0 : 0.0) : ((j == 10) ? (a == 2 ? -1.0 : 0.0) : 0.0);
-        }
-        double* out = C + s0 * 24;
-        double fin = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                xa[a] = (jq == 10) ? (a == 1 ? -1.0 : 0.0) : 0.0;
+                xb[a] = (jq == 9) ? (a == 0 ? -1.0 : 0.0) : ((jq == 10) ? (a == 2 ? -1.0 : 0.0) : 0.0);
+            }
+            double* out = C + sq * 24;
+            double fin = 0.0;
 #ifdef TGMS_BAND_NOBACK  // ablation build: forward elimination only
-        for (int k0 = kN; k0 >= 0 && false; k0 -= WC) {
+            for (int k0 = kN; k0 >= 0 && false; k0 -= WC) {
 #else
-        for (int k0 = kN; k0 >= 0; k0 -= WC) {
+            for (int k0 = kN; k0 >= 0; k0 -= WC) {
 #endif
-#define BSTEP(S) back_step<M, S>(k0 - S, j, g, rs, ur, xa, xb, out, live, emit, fin);
-            BSTEP(0) BSTEP(1) BSTEP(2) BSTEP(3) BSTEP(4) BSTEP(5) BSTEP(6) BSTEP(7) BSTEP(8) BSTEP(9)
-            BSTEP(10) BSTEP(11) BSTEP(12) BSTEP(13) BSTEP(14) BSTEP(15) BSTEP(16) BSTEP(17) BSTEP(18)
+#define BSTEP(S) back_step<M, S>(k0 - S, jq, slot, rs, ur, xa, xb, out, liveq, emit, fin);
+                BSTEP(0) BSTEP(1) BSTEP(2) BSTEP(3) BSTEP(4) BSTEP(5) BSTEP(6) BSTEP(7) BSTEP(8) BSTEP(9)
+                BSTEP(10) BSTEP(11) BSTEP(12) BSTEP(13) BSTEP(14) BSTEP(15) BSTEP(16) BSTEP(17) BSTEP(18)
 #undef BSTEP
-        }
-        const unsigned long long nf = __ballot(!(fin == 0.0));
-        const bool nonfinite = ((nf >> (QG * g)) & 0xffffull) != 0;
-        if (live && j == 0 && status) {
-            int32_t st = TGMS_OK;
-            if (!valid) st = TGMS_ERR_INVALID_ARG;
-            else if (singular) st = TGMS_ERR_SINGULAR;
-            else if (nonfinite) st = TGMS_ERR_NONFINITE;
-            status[b] = st;
+            }
+            const unsigned long long nf = __ballot(!(fin == 0.0));
+            const bool nonfinite = ((nf >> (QG * (lane / QG))) & 0xffffull) != 0;
+            if (liveq && jq == 0 && status) {
+                int32_t st = TGMS_OK;
+                if (!valid) st = TGMS_ERR_INVALID_ARG;
+                else if (singular) st = TGMS_ERR_SINGULAR;
+                else if (nonfinite) st = TGMS_ERR_NONFINITE;
+                status[bb] = st;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -562,8 +589,8 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
     }
     constexpr int kMaxBlocksPerCU = BAND_WAVES_PER_CU / QW;
     const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, kMaxBlocksPerCU);
-    const int32_t nquads = (n_traj + QT - 1) / QT;
-    const int32_t g = std::max<int32_t>(1, std::min<int32_t>(resident, (nquads + QW - 1) / QW));
+    const int32_t nocts = (n_traj + OT - 1) / OT;
+    const int32_t g = std::max<int32_t>(1, std::min<int32_t>(resident, (nocts + QW - 1) / QW));
     if (ED)
         TGMS_LAUNCH((k_band_kkt<M, true>), dim3(g), dim3(QW * W64), 0, stream, n_traj, ids, so, W, T, ED, C,
                     status, scratch);
@@ -573,7 +600,7 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
     return hipSuccess;
 }
 
-constexpr int SLABS_PER_WAVE = QT;
+constexpr int SLABS_PER_WAVE = OT;
 
 
 }  // namespace
