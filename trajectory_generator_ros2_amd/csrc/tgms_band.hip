@@ -11,16 +11,14 @@
 // that dense GEPP, not a band routine).  Flops: ~2 N kl (kl+ku) ~ 50 kflop at M = 10
 // against 2/3 N^3 = 1.9 MFLOP for the unordered dense LU (tgms_dense.hip).
 //
-// Mapping (gfx950): a 16-lane DPP row per trajectory, four per wavefront, four
-// wavefronts per workgroup (sharing the entry table).  Forward elimination keeps one
-// window row per lane (row_step below): DPP pivot search, LDS broadcast of the pivot row,
-// 21 FMAs per lane and step, the entering row k+10 assembled column-parallel from the
-// segment powers T_i^e and the 2Q blocks staged in LDS (a1/a2 never exist as a matrix).
-// Each finished U row (1/pivot, 18 super-diagonal entries, 3 eliminated right-hand
-// sides: 176 B) goes to a per-trajectory slab; back substitution (back_step) streams
-// the slab in reverse, a 16-B piece of a row per lane, as a DPP dot product.
-// Round 2's first mapping (a half-wavefront per trajectory, lane = window column) took
-// 2.50 ms per 65,536 at M = 10; this one 1.56 ms.
+// Mapping (gfx950, round 3): forward elimination by a quad of lanes per trajectory,
+// sixteen trajectories per wavefront, the whole 10 x 22 window in registers (quad_step
+// below: DPP pivot broadcast, in-register row selection by exact 0/1 masks, no LDS
+// traffic for window data); each finished U row, scaled by 1/pivot, goes to a
+// per-trajectory slab in slot order; back substitution (back_step) by 8-lane groups
+// reads it back 16 + 8 B per lane and row.  Round 2's row-lane mapping (a 16-lane DPP row
+// per trajectory, LDS pivot-row broadcast) took 1.56-1.61 ms per 65,536 at M = 10; this
+// one 1.33 ms.
 #include <algorithm>
 
 #include "tgms_device.h"
@@ -32,7 +30,7 @@ namespace {
 constexpr int KL = 9;              // sub-diagonals (== super-diagonals) of the interleaved KKT
 constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
-constexpr int UW = WC + 3;         // slab row: U row (19) + 3 eliminated right-hand sides
+constexpr int SW = 24;             // slab row: 19 window slots + 3 eliminated right-hand sides + 2 zeros
 
 // Position q of the interleaved order.  kind: 0 start row (idx = derivative k),
 // 1 coefficient (seg, idx = power j), 2 interior-knot row after segment seg
@@ -123,31 +121,52 @@ __device__ __forceinline__ double recip(double x) {
 }
 
 // ---------------------------------------------------------------------------
-// Octet mapping (round 3): eight lanes per trajectory in the forward elimination, eight
-// trajectories per wavefront.  Lane j < 5 holds TWO window rows, 2j and 2j+1: their
-// entries at columns k..k+18 in registers u[c mod 19] (static names under a 19-step
-// unroll) and their 3 right-hand sides.  Rows never move between lanes: the pivot search
-// is a DPP max over the octet (quad swaps and the half-row mirror), then the lowest
-// position among the maxima (ties to the lowest position in the permuted order, as
-// LAPACK and the oracle), the interchange swaps two position labels, and the pivot row
-// reaches the other lanes through one LDS broadcast that each lane reads once for both
-// of its rows.  The per-step work that does not grow with the rows -- pivot search,
-// pivot-row hand-over, entering row, bookkeeping -- is paid once per eight trajectories
-// (round 2's row-lane mapping: once per four, a 16-lane row per trajectory with one
-// window row per lane).  Back substitution keeps the 16-lane rows (four trajectories at
-// a time, two passes).
-constexpr int QG = 16;                  // back substitution: lanes per trajectory (one DPP row)
-constexpr int QT = W64 / QG;            // back substitution: trajectories per pass
-constexpr int OG = 8;                   // forward elimination: lanes per trajectory (half a DPP row)
-constexpr int OT = W64 / OG;            // trajectories per wavefront
-constexpr int OL = WR / 2;              // lanes holding window rows (two each)
-constexpr int QW = 4;                   // wavefronts per workgroup (share the entry table)
-constexpr int QS = UW + 2;              // LDS row stride of the pivot / entering rows (16-B aligned)
+// Quad mapping (round 3): four lanes per trajectory, sixteen trajectories per wavefront,
+// the whole 10-row window in registers.  Lane q of a trajectory's quad holds every
+// window row's entries in register slots s = 4 j + q (j = 0..5): slots 0..18 are the
+// window columns (column c in slot c mod 19, so a column leaves and the next one enters
+// the same slot and the 19-step unroll names every register statically), 19..21 the
+// three right-hand sides, 22..23 unused zeros.  Rows never move; a position label per
+// row records the interchanges.  A step k (R = k mod 19):
+//   - column k (slot R, one lane's register) is broadcast over the quad by a DPP
+//     quad_perm, so every lane finds the same pivot: the largest |a|, ties to the lowest
+//     position (as LAPACK and the oracle's KKT_BAND);
+//   - with m_r = [r is the pivot row] the pivot row is p = sum_r m_r u_r (exact: one
+//     term is nonzero) and the multipliers l_r = a_rk / a_pk with l_p = 1 exactly;
+//   - every row: u_r <- u_r - l_r p + m_r e, e the entering row k+10 -- the pivot row
+//     cancels exactly and takes the entering row, the others are eliminated, slot R
+//     restarts as column k+19 (zero outside the entering row);
+//   - the U row [1/pivot, columns k+1..k+18, rhs] goes to the trajectory's slab (8 B per
+//     lane and register), in the layout back_step reads.
+// The entering row is assembled per lane from the pattern table (coefficient, index
+// into the staged V of the row's segment) for its own slots.  No LDS traffic carries
+// window data; the per-step work is ~380 VALU instructions per wavefront = ~24 per
+// trajectory (round 2's row-lane mapping: ~50 VALU + ~50 SALU + 14 LDS per trajectory).
+constexpr int QL = 4;                   // forward elimination: lanes per trajectory
+constexpr int QTW = W64 / QL;           // trajectories per wavefront
+constexpr int NJ = 6;                   // registers per window row and lane (slots 4 j + q)
+constexpr int QW = 4;                   // wavefronts per workgroup (share the pattern table)
+// One wavefront per SIMD: the window (120 VGPRs), the masks, multipliers, pivot and
+// entering rows need ~290 registers; squeezed into 256 for two wavefronts per SIMD the
+// kernel spills, and the spilling build returned wrong results for the second workgroup
+// on a CU in measured runs, so the kernel runs at one wavefront per SIMD
+// with the AGPRs as register space and no scratch.
 #ifndef TGMS_BAND_WAVES_PER_EU
-#define TGMS_BAND_WAVES_PER_EU 2
+#define TGMS_BAND_WAVES_PER_EU 1
 #endif
 
-using gdouble = __attribute__((address_space(1))) double;  // global: keeps slab accesses off the flat path
+// Per-trajectory LDS block: Vc (the entering row's segment) | T | waypoints | end derivs.
+// Vc = [1, T^0..T^7 (0..8), 2 T^e / e for e = 1..7 (9..15), 0, 0, 0 (16..18)]
+constexpr int XV = 19;
+constexpr int XZ = 16;                  // first of the three zero slots
+__host__ __device__ constexpr int x_t(int) { return XV; }
+__host__ __device__ constexpr int x_w(int M) { return XV + M; }
+__host__ __device__ constexpr int x_e(int M) { return XV + M + 3 * (M + 1); }
+__host__ __device__ constexpr int x_len(int M) { return XV + M + 3 * (M + 1) + 18; }
+
+// pattern table entry: coefficient and Vc index of the entry at (row pattern, d + 9)
+__host__ __device__ constexpr int pack_d(int coef, int idx) { return coef * 256 + idx; }
+constexpr int NPAT = 4 * NOFF;          // (block variant, row offset) patterns
 
 template <int CTRL>
 __device__ __forceinline__ int dpp_i32(int v) {
@@ -161,42 +180,30 @@ __device__ __forceinline__ int opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
-__device__ __forceinline__ gdouble* opaque(gdouble* p) {
-    asm volatile("" : "+v"(p));
-    return p;
+
+// Vc of segment i from the staged T_i (one lane of the quad writes it)
+__device__ __forceinline__ void set_vc(int i, int q, double* X) {
+    if (q == 0) {
+        const double t = X[XV + i];
+        double pw = 1.0;
+        X[0] = 1.0;
+        X[1] = 1.0;
+#pragma unroll
+        for (int e = 1; e < 8; ++e) {
+            pw *= t;
+            X[1 + e] = pw;
+            X[8 + e] = 2.0 * (pw / (double)e);
+        }
+    }
 }
 
-// A row of the interleaved KKT from its structural nonzeros (at most NE = 10 per row):
-// a per-(block variant, row offset) list of (coefficient, diagonal offset, V index),
-// built once per workgroup from the entry table.
-constexpr int NE = 10;                  // structural nonzeros per row, at most
-constexpr int NPAT = 4 * NOFF;          // (variant, row offset) patterns
-
-__host__ __device__ constexpr int pack_ent(int coef, int d, int idx) { return (coef << 10) | ((d + KL) << 5) | idx; }
-
-// value of a packed entry of segment block vi (V_i = [1, T_i^0..T_i^7])
-__device__ __forceinline__ double ent_value(int e, const double* vi) {
-    const int idx = e & 31;
-    const double c = (double)(e >> 10);
-    if (idx < VAL) return c * vi[idx];
-    const int ex = idx - VAL;  // a 2Q_i entry: 2 (dfac dfac T^e / e), as the oracle forms it
-    return 2.0 * (c * vi[1 + ex] / (double)ex);
-}
-
-// Assemble row r (wave-uniform) into the octet's LDS row E in register-slot order:
-// column r + d goes to slot (base + d) mod 19 (base = r mod 19 when column c sits in
-// register c mod 19), the 3 right-hand sides to slots 19..21.  The octet's 8 lanes
-// zero the 22 slots (11 16-B writes), then lane j writes items j and j + 8 of the row's
-// 13 (10 nonzeros, 3 right-hand sides).  LDS operations of a wave execute in order, so
-// the zeros land before the items.
+// The row pattern (offset into the table) and the right-hand-side source (index into
+// X; the zero slots when the row has none) of interleaved-KKT row r (wave-uniform).
 template <int M, bool HAS_ED>
-__device__ __forceinline__ void assemble_row(int r, int base, int j, const int* ents, const double* val,
-                                             const double* w, const double* ed, double* E) {
-    constexpr int N = 14 * M + 2;
-    const bool live_r = r < N;
+__device__ __forceinline__ void row_info(int r, int& pat_off, int& rsrc, int& seg) {
     const int i = (r < 4) ? 0 : min((r - 4) / 14, M - 1);
-    const int o = live_r ? r - (4 + 14 * i) : 0;
-    int wr = -1, eb = -1;  // right-hand-side source (uniform): waypoint row, end-derivative base
+    const int o = r - (4 + 14 * i);
+    int wr = -1, eb = -1;
     if (o < 0) {
         if (o == -4) wr = 0;
         else eb = (o + 3) * 3;
@@ -210,212 +217,207 @@ __device__ __forceinline__ void assemble_row(int r, int base, int j, const int* 
         }
     }
     const int vv = (i == 0 ? 1 : 0) | (i == M - 1 ? 2 : 0);
-    double2* E2 = reinterpret_cast<double2*>(E);
-    E2[j] = make_double2(0.0, 0.0);
-    if (j < UW / 2 - OG) E2[OG + j] = make_double2(0.0, 0.0);
-    const int* list = ents + (vv * NOFF + o + 4) * NE;
-    const double* vi = val + i * VAL;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int n = j + OG * h;  // item n of 13
-        if (n < NE) {
-            const int e = list[n];
-            const int d = ((e >> 5) & 31) - KL;
-            int t = base + d;
-            t += (t < 0) ? WC : 0;
-            t -= (t >= WC) ? WC : 0;
-            if (live_r && e != 0) E[t] = ent_value(e, vi);
-        } else if (n < NE + 3) {
-            const int ax = n - NE;
-            const double rw = w[max(wr, 0) * 3 + ax];
-            const double re = HAS_ED ? ed[max(eb, 0) + ax] : 0.0;
-            const double rhs = (wr >= 0) ? rw : ((HAS_ED && eb >= 0) ? re : 0.0);
-            if (live_r) E[WC + ax] = rhs;
-        }
-    }
+    pat_off = (vv * NOFF + o + 4) * WC;
+    rsrc = (wr >= 0) ? x_w(M) + 3 * wr : ((HAS_ED && eb >= 0) ? x_e(M) + eb : XZ);
+    seg = i;
 }
 
-// Take the assembled row from E into registers (11 16-B reads).
-__device__ __forceinline__ void take_row(const double* E, double (&u)[WC], double (&rh)[3]) {
-    const double2* E2 = reinterpret_cast<const double2*>(E);
-#pragma unroll
-    for (int q = 0; q < 9; ++q) {
-        const double2 v = E2[q];
-        u[2 * q] = v.x;
-        u[2 * q + 1] = v.y;
+// This lane's register J of a row: slot s = 4 J + q.  Window slots hold the entry at
+// table column ((s - R1) mod 19) + DD0 (a diagonal offset + 9; outside 0..18: zero),
+// slot 19 + a the row's right-hand side a, slots 22..23 zero.
+template <int J, int R1, int DD0>
+__device__ __forceinline__ double row_entry(int q, int pat_off, int rsrc, const int* sd, const double* X) {
+    if (J == 5) {
+        const int xi = (q < 2) ? rsrc + 1 + q : XZ;
+        return X[xi];
     }
-    const double2 v9 = E2[9], v10 = E2[10];
-    u[18] = v9.x;
-    rh[0] = v9.y;
-    rh[1] = v10.x;
-    rh[2] = v10.y;
+    const int s = 4 * J + q;
+    int tt = s - R1 + WC;
+    tt -= (tt >= WC) ? WC : 0;
+    const int id = tt + DD0;
+    const bool ok = (DD0 == 0) || (id >= 0 && id < WC);
+    int de = sd[pat_off + (ok ? id : 0)];
+    de = ok ? de : pack_d(0, XZ);
+    int xi = de & 255;
+    double c = (double)(de >> 8);
+    if (J == 4) {
+        const bool rot = q < 3;
+        xi = rot ? xi : rsrc;
+        c = rot ? c : 1.0;
+    }
+    return c * X[xi];
 }
 
-// Hand a window row to the octet as U row k: [1/pivot, columns k+1..k+18, rhs].
-template <int R>
-__device__ __forceinline__ void put_pivot_row(double* P, double cv, const double (&u)[WC], const double (&rh)[3]) {
-    double2* P2 = reinterpret_cast<double2*>(P);
-    P2[0] = make_double2(recip(cv), u[(R + 1) % WC]);
-#pragma unroll
-    for (int q = 1; q < 9; ++q) P2[q] = make_double2(u[(R + 2 * q) % WC], u[(R + 2 * q + 1) % WC]);
-    P2[9] = make_double2(u[(R + 18) % WC], rh[0]);
-    P2[10] = make_double2(rh[1], rh[2]);
-}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int M, bool HAS_ED, int R>
-__device__ __forceinline__ void oct_step(int k, int j0, double (&u0)[WC], double (&u1)[WC], double (&r0)[3],
-                                         double (&r1)[3], int& pos0, int& pos1, bool& sing, double* P, double* E,
-                                         gdouble* U, const int* ents, const double* val, const double* w,
-                                         const double* ed) {
+__device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)[WR][NJ], int (&pos)[WR],
+                                          bool& sing, __amdgpu_buffer_rsrc_t rs, const uint32_t vrow,
+                                          const uint32_t vrow1, const int* sd, double* X) {
+    constexpr int N = 14 * M + 2;
+    constexpr int JR = R / 4, O = R % 4;
+    constexpr int BC = O * 0x55;        // quad_perm [O, O, O, O]
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    const int j = opaque(j0);
-    assemble_row<M, HAS_ED>(k + WR, (R + WR) % WC, j, ents, val, w, ed, E);  // the entering row
-    // pivot search in column k (register R) over the octet's ten window rows
-    const bool win = j < OL;
-    const double c0 = u0[R], c1 = u1[R];
-    const double a0 = fabs(c0), a1 = fabs(c1);
-    double m = win ? fmax(a0, a1) : -1.0;
-    m = fmax(m, dpp_f64<0xB1>(m));   // quad_perm [1,0,3,2]
-    m = fmax(m, dpp_f64<0x4E>(m));   // quad_perm [2,3,0,1]
-    m = fmax(m, dpp_f64<0x141>(m));  // row_half_mirror: the octet
-    const bool eq0 = win && a0 == m, eq1 = win && a1 == m;
-    int cp = min(eq0 ? pos0 : 0x7fffffff, eq1 ? pos1 : 0x7fffffff);
-    cp = min(cp, dpp_i32<0xB1>(cp));
-    cp = min(cp, dpp_i32<0x4E>(cp));
-    cp = min(cp, dpp_i32<0x141>(cp));
-    const bool piv0 = eq0 && pos0 == cp, piv1 = eq1 && pos1 == cp;
-    sing = sing || !(m > 0.0);
-    if (piv0) put_pivot_row<R>(P, c0, u0, r0);
-    if (piv1) put_pivot_row<R>(P, c1, u1, r1);
-    __builtin_amdgcn_wave_barrier();
-    // U row k to the slab: 11 16-B pieces over the octet's 8 lanes
+    const int q = opaque(q0);
+    // pivot search on this lane's register JR (meaningful in lane O, which holds column k):
+    // the largest |a|, ties to the lowest position
+    double m = fabs(u[0][JR]);
+#pragma unroll
+    for (int r = 1; r < WR; ++r) m = fmax(m, fabs(u[r][JR]));
+    int key = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) key = min(key, fabs(u[r][JR]) == m ? ((pos[r] << 4) | r) : 0x7fffffff);
+    sing = sing || (q == O && !(m > 0.0));
+    key = dpp_i32<BC>(key);  // lane O's pivot to the quad
+    const int ps = key & 15, cp = key >> 4;
+    double mr[WR];
+    double pv0 = 0.0, pv1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+        mr[r] = (ps == r) ? 1.0 : 0.0;
+        if (r & 1) pv1 = fma(mr[r], u[r][JR], pv1);
+        else pv0 = fma(mr[r], u[r][JR], pv0);
+    }
+    // 1/pivot, formed in lane O, to the quad
+    const double inv = dpp_f64<BC>(recip(pv0 + pv1));
+    // the pivot row
+    double p[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        double a = mr[0] * u[0][j], b = mr[1] * u[1][j];
+#pragma unroll
+        for (int r = 2; r < WR; r += 2) {
+            a = fma(mr[r], u[r][j], a);
+            b = fma(mr[r + 1], u[r + 1][j], b);
+        }
+        p[j] = a + b;
+    }
+    // U row k, scaled by 1/pivot, to the slab in slot order, laid out for 16-B accesses on
+    // both sides: slots (s, s + 8), s < 8, as a 16-B pair at 16 s; slot s + 16 at
+    // 128 + 8 s.  This lane's registers (0, 2) and (1, 3) are pairs, 4 and 5 singles;
+    // column k's own slot stores 0 (the back substitution never multiplies it)
     {
-        const double2* P2 = reinterpret_cast<const double2*>(P);
-        gdouble* Uk = U + (size_t)k * UW;
-        const double2 v = P2[j];
-        Uk[2 * j] = v.x;
-        Uk[2 * j + 1] = v.y;
-        if (j < UW / 2 - OG) {
-            const double2 v2 = P2[OG + j];
-            Uk[2 * (OG + j)] = v2.x;
-            Uk[2 * (OG + j) + 1] = v2.y;
-        }
-    }
-    // rank-1 update of both rows of every window lane (the pivot row with multiplier 0:
-    // it is replaced by the entering row below); column k leaves (register R becomes
-    // column k+19, zero outside the entering row)
-    if (win) {
-        double p[UW];
-        const double2* Pd = reinterpret_cast<const double2*>(P);
+        double v[NJ];
 #pragma unroll
-        for (int q = 0; q < UW / 2; ++q) {
-            const double2 v = Pd[q];
-            p[2 * q] = v.x;
-            p[2 * q + 1] = v.y;
+        for (int j = 0; j < NJ; ++j) v[j] = (j == JR && q == O) ? 0.0 : p[j] * inv;
+#ifndef TGMS_BAND_NOSTORE  // ablation build: no slab stores
+        const int so = k * (SW * 8);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[0], v[2])), rs, vrow, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[1], v[3])), rs, vrow + 64u, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[4]), rs, vrow1, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[5]), rs, vrow1 + 32u, so, 0);
+#else
+        asm volatile("" : : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]));
+#endif
+    }
+    // the entering row k + 10
+    double e[NJ];
+    const int re = k + WR;
+    if (re < N) {
+        int pat_off, rsrc, seg;
+        row_info<M, HAS_ED>(re, pat_off, rsrc, seg);
+        if (seg > 0 && re == 4 + 14 * seg) {  // first row of a new segment block
+            set_vc(seg, q, X);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
         }
-        const double l0 = piv0 ? 0.0 : c0 * p[0];
-        const double l1 = piv1 ? 0.0 : c1 * p[0];
+        constexpr int R1 = (R + 1) % WC;
+        e[0] = row_entry<0, R1, 0>(q, pat_off, rsrc, sd, X);
+        e[1] = row_entry<1, R1, 0>(q, pat_off, rsrc, sd, X);
+        e[2] = row_entry<2, R1, 0>(q, pat_off, rsrc, sd, X);
+        e[3] = row_entry<3, R1, 0>(q, pat_off, rsrc, sd, X);
+        e[4] = row_entry<4, R1, 0>(q, pat_off, rsrc, sd, X);
+        e[5] = row_entry<5, R1, 0>(q, pat_off, rsrc, sd, X);
+    } else {
 #pragma unroll
-        for (int d = 1; d < WC; ++d) {
-            u0[(R + d) % WC] = fma(-l0, p[d], u0[(R + d) % WC]);
-            u1[(R + d) % WC] = fma(-l1, p[d], u1[(R + d) % WC]);
-        }
+        for (int j = 0; j < NJ; ++j) e[j] = 0.0;
+    }
+    // rank-1 update; the pivot row cancels exactly and takes the entering row; column k
+    // (lane O, register JR) restarts as column k + 19
+    const double keep = (q == O) ? 0.0 : 1.0;
+    p[JR] *= keep;
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            r0[a] = fma(-l0, p[WC + a], r0[a]);
-            r1[a] = fma(-l1, p[WC + a], r1[a]);
+    for (int r = 0; r < WR; ++r) {
+        // multiplier a_rk / a_pk (l_p = 1 exactly), formed in lane O (row r's column k is
+        // still unchanged there), to the quad
+        const double lr = dpp_f64<BC>(fma((ps == r) ? 0.0 : 1.0, u[r][JR] * inv, mr[r]));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const double base = (j == JR) ? u[r][j] * keep : u[r][j];
+            u[r][j] = fma(mr[r], e[j], fma(-lr, p[j], base));
         }
     }
-    u0[R] = 0.0;
-    u1[R] = 0.0;
-    if (pos0 == k) pos0 = cp;  // interchange: the row at position k takes the pivot's position
-    if (pos1 == k) pos1 = cp;
-    if (piv0) {  // the pivot's lane takes row k+WR into the pivot's slot
-        take_row(E, u0, r0);
-        pos0 = k + WR;
+    // interchange: the row at position k takes the pivot's position; the pivot's slot
+    // holds row k + 10 now
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+        int v = pos[r];
+        v = (v == k) ? cp : v;
+        pos[r] = (ps == r) ? re : v;
     }
-    if (piv1) {
-        take_row(E, u1, r1);
-        pos1 = k + WR;
-    }
-    __builtin_amdgcn_wave_barrier();  // P and E are rewritten by the next step
 }
 
-// Back substitution of one trajectory by its 16-lane row, row oriented:
-//   x_k = (b'_k - sum_{d=1..18} U[k][k+d] x_{k+d}) / U[k][k].
-// Lane j < 11 holds 16 B of U row k, (U[k][2j], U[k][2j+1]), and the matching window
-// values (x_{k+2j}, x_{k+2j+1}) for 3 axes; the dot product is a DPP butterfly over the
-// row.  The eliminated right-hand side rides in the same sum: lanes 9 and 10 hold the
-// constants -e_a against U[k][19..21], and lane 0's x_k slot is 0 against 1/U[k][k].
-// Lane 0 finalizes x_k = -sum * (1/U[k][k]) and the window slides one position (DPP
-// row shift), so x_k never leaves the registers.  Rows come through a 19-deep ring of
-// 16-B buffer loads issued one lap ahead (every ring slot its own register, every lane
-// loading: no load result is read before its lap is over).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Back substitution, eight lanes per trajectory, slot order.  Lane l holds slots l, l+8,
+// l+16 of the scaled U row k (one 16-B and one 8-B buffer load) and of the solution
+// window: x_c lives in slot c mod 19 for as long as it is in the band, the right-hand-side
+// slots 19..21 hold the constants -1 of their axis, slots 22..23 zero.  Then
+//   x_k = -sum_s U'[k][s] x[s]      (U' = U / pivot; slot k mod 19 stored as 0)
+// is a three-FMA partial per lane and axis and a DPP butterfly over the eight lanes; the
+// lane of slot k mod 19 keeps x_k (it replaces x_{k+19}, which left the band).  Rows come
+// through a 19-deep ring of loads issued one lap ahead (every ring slot its own
+// registers).
 constexpr int BCPOL_SC1 = 16;  // agent-scope (L1-bypassing) load: the slab was written by this wave
+constexpr int BL = 8;          // back substitution: lanes per trajectory
+constexpr int BT = W64 / BL;   // back substitution: trajectories per pass
 
-template <bool BOUND_ZERO>
-__device__ __forceinline__ double dpp_shr1_f64(double v) {
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x111, 0xF, 0xF, BOUND_ZERO);  // row_shr:1
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xF, 0xF, BOUND_ZERO);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+// byte offset of row kk of slab g (rows before 0: out of range, read as 0)
+__device__ __forceinline__ uint32_t slot_off(int g, int kk, int N) {
+    return (kk >= 0) ? (uint32_t)((g * N + kk) * SW * 8) : 0x7FFFFF00u;
 }
 
-__device__ __forceinline__ double2 ld_row16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, BCPOL_SC1));
-}
-
-// byte offset of lane j's 16 B of row kk in the wave's slabs (out of range: 0 returned)
-__device__ __forceinline__ uint32_t row_off(int g, int j, int kk, int N) {
-    return (kk >= 0 && j < UW / 2) ? (uint32_t)(((g * N + kk) * UW + 2 * j) * 8) : 0xFFFFFFF0u;
+// lane l's slots of a row: (l, l + 8) at 16 l, l + 16 at 128 + 8 l
+__device__ __forceinline__ void ld_slots(__amdgpu_buffer_rsrc_t rs, uint32_t row, int l, double2& a, double& b) {
+    a = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, row + 16u * l, 0, BCPOL_SC1));
+    b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, row + 128u + 8u * l, 0, BCPOL_SC1));
 }
 
 template <int M, int S>
-__device__ __forceinline__ void back_step(int k, int j0, int g, __amdgpu_buffer_rsrc_t rs, double2 (&ur)[WC],
-                                          double (&xa)[3], double (&xb)[3], double* out, bool live, bool emit,
+__device__ __forceinline__ void back_step(int k, int l0, int g, __amdgpu_buffer_rsrc_t rs, double2 (&ra)[WC],
+                                          double (&rb)[WC], double (&x)[3][3], double* out, bool live, bool emit,
                                           double& fin) {
     constexpr int N = 14 * M + 2;
+    constexpr int R = ((N - 1 - S) % WC + WC) % WC;  // slot of column k
+    constexpr int RI = R / BL, RL = R % BL;
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    const int j = opaque(j0);
-    const double2 uk = ur[S];
+    const int l = opaque(l0);
+    const double2 ua = ra[S];
+    const double ub = rb[S];
     double sm[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) sm[a] = fma(uk.y, xb[a], uk.x * xa[a]);
+    for (int a = 0; a < 3; ++a) sm[a] = fma(ub, x[2][a], fma(ua.y, x[1][a], ua.x * x[0][a]));
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         sm[a] += dpp_f64<0xB1>(sm[a]);   // quad_perm [1,0,3,2]
         sm[a] += dpp_f64<0x4E>(sm[a]);   // quad_perm [2,3,0,1]
-        sm[a] += dpp_f64<0x141>(sm[a]);  // row_half_mirror
-        sm[a] += dpp_f64<0x140>(sm[a]);  // row_mirror
+        sm[a] += dpp_f64<0x141>(sm[a]);  // row_half_mirror: the eight lanes
     }
-    // lane 0: uk.x = 1 / U[k][k]
-    double x[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) x[a] = -sm[a] * uk.x;
-    if (j == 0 && k >= 0) {
-        fin += (x[0] + x[1] + x[2]) * 0.0;
+    for (int a = 0; a < 3; ++a) x[RI][a] = (l == RL) ? -sm[a] : x[RI][a];
+    if (l == 0 && k >= 0) {
+        fin += (sm[0] + sm[1] + sm[2]) * 0.0;
         const Pos pk = decode<M>(k);
         if (pk.kind == 1 && live) {
             double* o = out + pk.seg * 24 + pk.idx;
-            o[0] = emit ? x[0] : 0.0;
-            o[8] = emit ? x[1] : 0.0;
-            o[16] = emit ? x[2] : 0.0;
+            o[0] = emit ? -sm[0] : 0.0;
+            o[8] = emit ? -sm[1] : 0.0;
+            o[16] = emit ? -sm[2] : 0.0;
         }
     }
-    // slide the window: (x_{k+2j}, x_{k+2j+1}) -> (x_{k-1+2j}, x_{k+2j}); lanes 9 and 10
-    // keep the right-hand-side constants
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double cur = (j == 0) ? x[a] : xa[a];
-        const double nxa = dpp_shr1_f64<true>(xb[a]);
-        xb[a] = (j == 9) ? (a == 0 ? -1.0 : 0.0) : ((j == 10) ? (a == 2 ? -1.0 : 0.0) : cur);
-        xa[a] = (j == 10) ? (a == 1 ? -1.0 : 0.0) : nxa;
-    }
     // refill the ring slot for step k-19 (same slot)
-    ur[S] = ld_row16(rs, row_off(g, j, k - WC, N));
+    ld_slots(rs, slot_off(g, k - WC, N), l, ra[S], rb[S]);
 }
 
 template <int M, bool HAS_ED>
@@ -424,129 +426,119 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     const double* __restrict__ W, const double* __restrict__ T, const double* __restrict__ ED, double* __restrict__ C,
     int32_t* __restrict__ status, double* __restrict__ scratch) {
     constexpr int N = 14 * M + 2;
-    __shared__ int s_ents[NPAT * NE];                        // per-row nonzero lists of the interleaved KKT
-    __shared__ double s_val[QW][OT][M * VAL];                // V_i = [1, T_i^0..T_i^7] per segment
-    __shared__ double s_w[QW][OT][(M + 1) * 3];              // waypoints
-    __shared__ double s_ed[QW][OT][HAS_ED ? 18 : 1];         // end derivatives
-    __shared__ alignas(16) double s_piv[QW][OT][QS];         // pivot row of the current step
-    __shared__ alignas(16) double s_ent[QW][OT][QS];         // entering row of the current step
+    constexpr int XL = x_len(M);
+    __shared__ int s_desc[NPAT * WC];                  // pattern table of the interleaved KKT
+    __shared__ double s_x[QW][QTW][XL];                // per-trajectory Vc | T | W | ED
 
-    const int wv = threadIdx.x / W64, lane = threadIdx.x % W64, g = lane / OG;
-    for (int q = threadIdx.x; q < NPAT; q += QW * W64) {
-        const int vv = q / NOFF, o = q % NOFF - 4;
-        int n = 0;
-        for (int d = -KL; d <= KL; ++d) {
-            const int de = desc_entry(vv, o, d);
-            if (de != 0 && n < NE) s_ents[q * NE + n++] = pack_ent(de >> 5, d, de & 31);
-        }
-        for (; n < NE; ++n) s_ents[q * NE + n] = 0;
+    for (int n = threadIdx.x; n < NPAT * WC; n += QW * W64) {
+        const int pat = n / WC, d = n % WC - KL;
+        const int vv = pat / NOFF, o = pat % NOFF - 4;
+        const int de = desc_entry(vv, o, d);
+        const int idx = de & 31;
+        s_desc[n] = (de == 0) ? pack_d(0, XZ) : pack_d(de >> 5, idx < VAL ? idx : idx - 1);
     }
     __syncthreads();
-    const int wave_id = blockIdx.x * QW + wv;
-    gdouble* const U0 = (gdouble*)scratch + ((size_t)wave_id * OT + g) * (size_t)N * UW;
-    double* val = s_val[wv][g];
-    double* w = s_w[wv][g];
-    double* ed = s_ed[wv][g];
-    double* P = s_piv[wv][g];
-    double* E = s_ent[wv][g];
-    const int nocts = (n_traj + OT - 1) / OT;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / W64), lane = threadIdx.x % W64, g = lane / QL;
+    const int wave_id = blockIdx.x * QW + wv;  // wave-uniform (SGPR): the slab resource stays scalar
+    double* const X = s_x[wv][g];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        scratch + (size_t)wave_id * QTW * N * SW, (short)0, QTW * N * SW * 8, 0x00020000);
+    // this lane's places in a slab row: its pairs at 16 q (+ 64), its singles at 128 + 8 q (+ 32)
+    const uint32_t vrow = (uint32_t)(g * N * SW * 8 + 16 * (lane % QL));
+    const uint32_t vrow1 = (uint32_t)(g * N * SW * 8 + 128 + 8 * (lane % QL));
+    const int ngroups = (n_traj + QTW - 1) / QTW;
 
-    for (int oc = wave_id; oc < nocts; oc += gridDim.x * QW) {
-        // per-octet opaque copies: the slab addresses must not be hoisted out of this loop
-        gdouble* const U = opaque(U0);
-        const int j = opaque(lane % OG);
-        const int bi = OT * oc + g;
+    for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
+        const int q = opaque(lane % QL);
+        const int bi = QTW * grp + g;
         const bool live = bi < n_traj;
-        const int32_t b = ids ? ids[live ? bi : OT * oc] : (live ? bi : OT * oc);
+        const int32_t b = ids ? ids[live ? bi : QTW * grp] : (live ? bi : QTW * grp);
         const int64_t s0 = seg_offsets ? (int64_t)seg_offsets[b] : (int64_t)b * M;
         const double* gw = W + (s0 + b) * 3;
         const double* gt = T + s0;
 
         // ---- stage inputs, validate (T > 0 finite; W, ED finite)
         bool ok = true;
-        for (int q = j; q < (M + 1) * 3; q += OG) {
-            const double v = gw[q];
-            w[q] = v;
+        for (int n = q; n < (M + 1) * 3; n += QL) {
+            const double v = gw[n];
+            X[x_w(M) + n] = v;
             ok = ok && (v * 0.0 == 0.0);
         }
         if (HAS_ED) {
-            for (int q = j; q < 18; q += OG) {
-                const double v = ED[(int64_t)b * 18 + q];
-                ed[q] = v;
+            for (int n = q; n < 18; n += QL) {
+                const double v = ED[(int64_t)b * 18 + n];
+                X[x_e(M) + n] = v;
                 ok = ok && (v * 0.0 == 0.0);
             }
         }
-        for (int i = j; i < M; i += OG) {
+        for (int i = q; i < M; i += QL) {
             const double t = gt[i];
             ok = ok && finite_pos(t);
-            double p = 1.0;
-            val[i * VAL] = 1.0;
-            val[i * VAL + 1] = 1.0;
-#pragma unroll
-            for (int e = 1; e < 8; ++e) {
-                p *= t;
-                val[i * VAL + 1 + e] = p;
-            }
+            X[x_t(M) + i] = t;
         }
-        const unsigned long long badm = __ballot(!ok);  // 8 bits per octet
+        if (q < 3) X[XZ + q] = 0.0;
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        set_vc(0, q, X);
+        const unsigned long long badm = __ballot(!ok);  // 4 bits per trajectory
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
 
-        // ---- the initial window: rows 0..9, assembled through E one at a time; lane
-        // j < 5 takes rows 2j (u0) and 2j+1 (u1)
-        double u0[WC], u1[WC], r0[3], r1[3];
-#pragma unroll
-        for (int rr = 0; rr < WR; ++rr) {
-            assemble_row<M, HAS_ED>(rr, rr, j, s_ents, val, w, ed, E);
-            __builtin_amdgcn_wave_barrier();
-            if (j == rr / 2) {
-                if (rr & 1)
-                    take_row(E, u1, r1);
-                else
-                    take_row(E, u0, r0);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        int pos0 = (j < OL) ? 2 * j : -1, pos1 = (j < OL) ? 2 * j + 1 : -1;  // positions in the permuted order
+        // ---- the initial window: rows 0..9 over columns 0..18 (slot s = column s)
+        double u[WR][NJ];
+        int pos[WR];
+#define IROW(RR)                                                                      \
+    {                                                                                 \
+        int pat_off, rsrc, seg;                                                       \
+        row_info<M, HAS_ED>(RR, pat_off, rsrc, seg);                                  \
+        u[RR][0] = row_entry<0, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        u[RR][1] = row_entry<1, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        u[RR][2] = row_entry<2, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        u[RR][3] = row_entry<3, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        u[RR][4] = row_entry<4, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        u[RR][5] = row_entry<5, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
+        pos[RR] = RR;                                                                 \
+    }
+        IROW(0) IROW(1) IROW(2) IROW(3) IROW(4) IROW(5) IROW(6) IROW(7) IROW(8) IROW(9)
+#undef IROW
         bool sing = false;
 
         // ---- forward elimination (a3)
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) oct_step<M, HAS_ED, R>(k0 + R, j, u0, u1, r0, r1, pos0, pos1, sing, P, E, U, s_ents, val, w, ed);
+    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, pos, sing, rs, vrow, vrow1, s_desc, X);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
         }
         const unsigned long long singm = __ballot(sing);
 
-        // ---- back substitution, 16-lane rows, four trajectories per pass.  The U rows
+        // ---- back substitution, 8-lane groups, eight trajectories per pass.  The U rows
         // this wave stored are read back by other lanes of the wave: wait for the stores to
         // reach L2 and read them with L1-bypassing loads (the slab is reused by the next
-        // octet, so L1 may hold the previous one's lines)
+        // group, so L1 may hold the previous one's lines)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         constexpr int kN = N - 1;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            scratch + (size_t)wave_id * OT * N * UW, (short)0, OT * N * UW * 8, 0x00020000);
-        const int jq = opaque(lane % QG);
+        const int lb = opaque(lane % BL);
 #pragma unroll 1
-        for (int pass = 0; pass < OT / QT; ++pass) {
-            const int slot = pass * QT + lane / QG;  // trajectory slot of this 16-lane row
-            const int bq = OT * oc + slot;
+        for (int pass = 0; pass < QTW / BT; ++pass) {
+            const int slot = pass * BT + lane / BL;  // trajectory slot of this 8-lane group
+            const int bq = QTW * grp + slot;
             const bool liveq = bq < n_traj;
-            const int32_t bb = ids ? ids[liveq ? bq : OT * oc] : (liveq ? bq : OT * oc);
+            const int32_t bb = ids ? ids[liveq ? bq : QTW * grp] : (liveq ? bq : QTW * grp);
             const int64_t sq = seg_offsets ? (int64_t)seg_offsets[bb] : (int64_t)bb * M;
-            const bool valid = ((badm >> (OG * slot)) & 0xffull) == 0;
-            const bool singular = ((singm >> (OG * slot)) & 0xffull) != 0;
+            const bool valid = ((badm >> (QL * slot)) & 0xfull) == 0;
+            const bool singular = ((singm >> (QL * slot)) & 0xfull) != 0;
             const bool emit = liveq && valid && !singular;
-            double2 ur[WC];
+            double2 ra[WC];
+            double rb[WC];
 #pragma unroll
-            for (int S = 0; S < WC; ++S) ur[S] = ld_row16(rs, row_off(slot, jq, kN - S, N));
-            double xa[3], xb[3];
+            for (int S = 0; S < WC; ++S) ld_slots(rs, slot_off(slot, kN - S, N), lb, ra[S], rb[S]);
+            double x[3][3];
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                xa[a] = (jq == 10) ? (a == 1 ? -1.0 : 0.0) : 0.0;
-                xb[a] = (jq == 9) ? (a == 0 ? -1.0 : 0.0) : ((jq == 10) ? (a == 2 ? -1.0 : 0.0) : 0.0);
-            }
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) x[i][a] = (i == 2 && lb == 3 + a) ? -1.0 : 0.0;
             double* out = C + sq * 24;
             double fin = 0.0;
 #ifdef TGMS_BAND_NOBACK  // ablation build: forward elimination only
@@ -554,14 +546,14 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
 #else
             for (int k0 = kN; k0 >= 0; k0 -= WC) {
 #endif
-#define BSTEP(S) back_step<M, S>(k0 - S, jq, slot, rs, ur, xa, xb, out, liveq, emit, fin);
+#define BSTEP(S) back_step<M, S>(k0 - S, lb, slot, rs, ra, rb, x, out, liveq, emit, fin);
                 BSTEP(0) BSTEP(1) BSTEP(2) BSTEP(3) BSTEP(4) BSTEP(5) BSTEP(6) BSTEP(7) BSTEP(8) BSTEP(9)
                 BSTEP(10) BSTEP(11) BSTEP(12) BSTEP(13) BSTEP(14) BSTEP(15) BSTEP(16) BSTEP(17) BSTEP(18)
 #undef BSTEP
             }
             const unsigned long long nf = __ballot(!(fin == 0.0));
-            const bool nonfinite = ((nf >> (QG * (lane / QG))) & 0xffffull) != 0;
-            if (liveq && jq == 0 && status) {
+            const bool nonfinite = ((nf >> (BL * (lane / BL))) & 0xffull) != 0;
+            if (liveq && lb == 0 && status) {
                 int32_t st = TGMS_OK;
                 if (!valid) st = TGMS_ERR_INVALID_ARG;
                 else if (singular) st = TGMS_ERR_SINGULAR;
@@ -569,6 +561,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
                 status[bb] = st;
             }
         }
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -579,7 +572,7 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
                   hipStream_t stream) {
     if (n_traj <= 0) return hipSuccess;
     // persistent grid of resident workgroups only (a second, partial round would double
-    // the tail); `grid` counts wavefronts, each with QT slabs
+    // the tail); `grid` counts wavefronts, each with QTW slabs
     static int occ[2] = {0, 0};
     int& nb = occ[ED ? 1 : 0];
     if (nb == 0) {
@@ -589,8 +582,8 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
     }
     constexpr int kMaxBlocksPerCU = BAND_WAVES_PER_CU / QW;
     const int32_t resident = (grid / BAND_WAVES_PER_CU) * std::min(nb, kMaxBlocksPerCU);
-    const int32_t nocts = (n_traj + OT - 1) / OT;
-    const int32_t g = std::max<int32_t>(1, std::min<int32_t>(resident, (nocts + QW - 1) / QW));
+    const int32_t ngroups = (n_traj + QTW - 1) / QTW;
+    const int32_t g = std::max<int32_t>(1, std::min<int32_t>(resident, (ngroups + QW - 1) / QW));
     if (ED)
         TGMS_LAUNCH((k_band_kkt<M, true>), dim3(g), dim3(QW * W64), 0, stream, n_traj, ids, so, W, T, ED, C,
                     status, scratch);
@@ -600,13 +593,10 @@ hipError_t band_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const d
     return hipSuccess;
 }
 
-constexpr int SLABS_PER_WAVE = OT;
-
-
 }  // namespace
 
 size_t band_scratch_bytes(int M, int32_t grid) {
-    return (size_t)grid * SLABS_PER_WAVE * (size_t)(14 * M + 2) * UW * sizeof(double);
+    return (size_t)grid * QTW * (size_t)(14 * M + 2) * SW * sizeof(double);
 }
 
 hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* ids, const int32_t* so, const double* W,
