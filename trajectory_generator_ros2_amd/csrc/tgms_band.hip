@@ -30,7 +30,7 @@ namespace {
 constexpr int KL = 9;              // sub-diagonals (== super-diagonals) of the interleaved KKT
 constexpr int WR = KL + 1;         // window rows
 constexpr int WC = 2 * KL + 1;     // window columns == width of a U row (diagonal + kl+ku)
-constexpr int SW = 24;             // slab row: 19 window slots + 3 eliminated right-hand sides + 2 zeros
+constexpr int SW = 22;             // slab row: 19 window slots + 3 eliminated right-hand sides (176 B)
 
 // Position q of the interleaved order.  kind: 0 start row (idx = derivative k),
 // 1 coefficient (seg, idx = power j), 2 interior-knot row after segment seg
@@ -254,7 +254,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <int M, bool HAS_ED, int R>
 __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)[WR][NJ], int (&pos)[WR],
                                           bool& sing, __amdgpu_buffer_rsrc_t rs, const uint32_t vrow,
-                                          const uint32_t vrow1, const int* sd, double* X) {
+                                          const uint32_t vrow1, const uint32_t vrow5, const int* sd, double* X) {
     constexpr int N = 14 * M + 2;
     constexpr int JR = R / 4, O = R % 4;
     constexpr int BC = O * 0x55;        // quad_perm [O, O, O, O]
@@ -295,7 +295,7 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         p[j] = a + b;
     }
     // U row k, scaled by 1/pivot, to the slab in slot order, laid out for 16-B accesses on
-    // both sides: slots (s, s + 8), s < 8, as a 16-B pair at 16 s; slot s + 16 at
+    // both sides: slots (s, s + 8), s < 8, as a 16-B pair at 16 s; slot s + 16 (s < 6) at
     // 128 + 8 s.  This lane's registers (0, 2) and (1, 3) are pairs, 4 and 5 singles;
     // column k's own slot stores 0 (the back substitution never multiplies it)
     {
@@ -307,7 +307,7 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[0], v[2])), rs, vrow, so, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[1], v[3])), rs, vrow + 64u, so, 0);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[4]), rs, vrow1, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[5]), rs, vrow1 + 32u, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[5]), rs, vrow5, so, 0);
 #else
         asm volatile("" : : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]));
 #endif
@@ -377,10 +377,12 @@ __device__ __forceinline__ uint32_t slot_off(int g, int kk, int N) {
     return (kk >= 0) ? (uint32_t)((g * N + kk) * SW * 8) : 0x7FFFFF00u;
 }
 
-// lane l's slots of a row: (l, l + 8) at 16 l, l + 16 at 128 + 8 l
+// lane l's slots of a row: (l, l + 8) at 16 l, l + 16 at 128 + 8 l (slots 22, 23, lanes 6
+// and 7, are not stored: read as 0 through an out-of-range offset)
 __device__ __forceinline__ void ld_slots(__amdgpu_buffer_rsrc_t rs, uint32_t row, int l, double2& a, double& b) {
     a = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, row + 16u * l, 0, BCPOL_SC1));
-    b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, row + 128u + 8u * l, 0, BCPOL_SC1));
+    const uint32_t o1 = (l < 6 && row < 0x7FFFFF00u) ? row + 128u + 8u * l : 0x7FFFFF00u;
+    b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, BCPOL_SC1));
 }
 
 template <int M, int S>
@@ -446,6 +448,9 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     // this lane's places in a slab row: its pairs at 16 q (+ 64), its singles at 128 + 8 q (+ 32)
     const uint32_t vrow = (uint32_t)(g * N * SW * 8 + 16 * (lane % QL));
     const uint32_t vrow1 = (uint32_t)(g * N * SW * 8 + 128 + 8 * (lane % QL));
+    // register 5: the right-hand sides 1 and 2 (lanes 0, 1); lanes 2, 3 hold the unused
+    // slots 22, 23, which the slab does not keep (an out-of-range offset drops the store)
+    const uint32_t vrow5 = (lane % QL < 2) ? vrow1 + 32u : 0x7FFFFF00u;
     const int ngroups = (n_traj + QTW - 1) / QTW;
 
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
@@ -506,7 +511,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         // ---- forward elimination (a3)
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, pos, sing, rs, vrow, vrow1, s_desc, X);
+    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, pos, sing, rs, vrow, vrow1, vrow5, s_desc, X);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
