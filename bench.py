@@ -155,48 +155,39 @@ def cpu_baseline(B: int, M: int, target_s: float):
 C5_PMC_FILE = "profiles/c5_pmc.json"
 
 
-def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_T=1.0, eta=0.1, reps=5):
-    """Config 5: a 1,048,576-trajectory ragged batch (M ~ U{2..16}) split over 8 GPUs
-    (the configuration's count, whatever N is) into contiguous cost-balanced shards
-    (shard.ragged_bounds); this rank solves shard `rank % 8`: `iters` time-refinement
-    steps + the final solve, one tgms_refine_loop_device call (planned once).
-    `ms_per_batch` is the median of HIP-event pairs around single calls on the launch
-    stream (the times are reset from a device copy before each call, outside the
-    events); the wall clock per call (host planning included) is beside it.
-
-    Roofline: the loop is FP64-VALU-bound.  `achieved` = the executed FP64 flops of one
-    call (committed PMC, profiles/c5_pmc.json) / the live event time, against the FP64
-    vector peak; the algorithmic HBM bytes (waypoints + times read, times + coefficients
-    + costs + statuses written) and their rate are beside it."""
+def _c5_shard(so_all, W_all, T_all, bounds, part, dev):
+    """Shard `part` of the config-5 batch, resident on `dev`."""
     import torch
     from trajectory_generator_ros2_amd import shard as SH
-    from trajectory_generator_ros2_amd import synthetic as S
-    so_all, W_all, T_all = S.ragged_batch(B_total, 2, 16)
-    bounds = SH.ragged_bounds(so_all, 8)
-    part = rank % 8
     so, W, T, _ = SH.shard_csr(so_all, W_all, T_all, None, int(bounds[part]), int(bounds[part + 1]))
-    del so_all, W_all, T_all
     B = len(so) - 1
     Sg = int(so[-1])
-    d_so = torch.from_numpy(so.astype(np.int32)).to(dev)
-    dW = torch.from_numpy(W.reshape(-1, 3)).to(dev)
-    T0 = torch.from_numpy(T.reshape(-1)).to(dev)
-    dT = torch.empty_like(T0)
+    return {"so": so, "B": B, "Sg": Sg, "d_so": torch.from_numpy(so.astype(np.int32)).to(dev),
+            "dW": torch.from_numpy(W.reshape(-1, 3)).to(dev), "T0": torch.from_numpy(T.reshape(-1)).to(dev)}
+
+
+def _c5_time(solver, sh, dev, stream, iters, k_T, eta, reps):
+    """Median HIP-event time of one tgms_refine_loop_device call over shard `sh` (times
+    reset from a device copy before each call, outside the events), the wall time per
+    call, and the statuses of the last call."""
+    import torch
+    so, B, Sg = sh["so"], sh["B"], sh["Sg"]
+    dT = torch.empty_like(sh["T0"])
     dC = torch.empty((Sg, 3, 8), dtype=torch.float64, device=dev)
     dcost = torch.empty(B, dtype=torch.float64, device=dev)
     dst = torch.empty(B, dtype=torch.int32, device=dev)
     sp = stream.cuda_stream
 
     def call():
-        solver.refine_loop_device(so, d_so, dW, dT, k_T, eta, iters, dC, dcost, dst, stream=sp)
+        solver.refine_loop_device(so, sh["d_so"], sh["dW"], dT, k_T, eta, iters, dC, dcost, dst, stream=sp)
 
     for _ in range(2):
-        dT.copy_(T0)
+        dT.copy_(sh["T0"])
         call()
     torch.cuda.synchronize()
     evs = []
     for _ in range(reps):
-        dT.copy_(T0)
+        dT.copy_(sh["T0"])
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         call()
@@ -206,17 +197,59 @@ def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_
     ms = sorted(a.elapsed_time(b) for a, b in evs)[reps // 2]
     t0 = time.perf_counter()
     for _ in range(reps):
-        dT.copy_(T0)
+        dT.copy_(sh["T0"])
         call()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / reps * 1e3
-    assert int((dst != 0).sum().item()) == 0, "refinement reported failures"
+    return ms, wall, int((dst != 0).sum().item())
+
+
+def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_T=1.0, eta=0.1, reps=5):
+    """Config 5: a 1,048,576-trajectory ragged batch (M ~ U{2..16}) split over 8 GPUs
+    (the configuration's count, whatever N is) into contiguous cost-balanced shards
+    (shard.ragged_bounds); this rank solves shard `rank % 8`: `iters` time-refinement
+    steps + the final solve, one tgms_refine_loop_device call (planned once).
+    `ms_per_batch` is the median of HIP-event pairs around single calls on the launch
+    stream (the times are reset from a device copy before each call, outside the
+    events); the wall clock per call (host planning included) is beside it.
+
+    Shard balance: at N = 1 every one of the 8 shards is timed the
+    same way on this GPU, one after another; `shard_balance` = max / mean of those times
+    (at N = 8 the config-5 time is the slowest shard's).
+
+    Roofline: the loop is FP64-VALU-bound.  `achieved` = the executed FP64 flops of one
+    call (committed PMC, profiles/c5_pmc.json) / the live event time, against the FP64
+    vector peak; the algorithmic HBM bytes (waypoints + times read, times + coefficients
+    + costs + statuses written) and their rate are beside it."""
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd import synthetic as S
+    so_all, W_all, T_all = S.ragged_batch(B_total, 2, 16)
+    bounds = SH.ragged_bounds(so_all, 8)
+    part = rank % 8
+    sh = _c5_shard(so_all, W_all, T_all, bounds, part, dev)
+    B, Sg = sh["B"], sh["Sg"]
+    ms, wall, bad = _c5_time(solver, sh, dev, stream, iters, k_T, eta, reps)
+    assert bad == 0, "refinement reported failures"
+    shard_ms = None
+    if world == 1:
+        shard_ms = []
+        for p in range(8):
+            shp = sh if p == part else _c5_shard(so_all, W_all, T_all, bounds, p, dev)
+            m_p, _, bad = _c5_time(solver, shp, dev, stream, iters, k_T, eta, 3)
+            assert bad == 0, "refinement reported failures"
+            shard_ms.append(m_p)
+            del shp
+    del so_all, W_all, T_all
     nbytes = (Sg + B) * 24 + 2 * Sg * 8 + Sg * 192 + B * (8 + 4) + (B + 1) * 4
     line = {"workload": f"config5: shard {part} of 8 (cost-balanced, {B} trajectories) of a {B_total}-trajectory "
                         f"ragged batch, M~U{{2..16}}, {iters} refinement steps + final solve",
             "ms_per_batch": ms, "ms_wall_per_call": wall, "trajectories_per_s": B / (ms * 1e-3), "segments": Sg,
             "k_T": k_T, "eta": eta,
             "timing": "median of single-call HIP event pairs on the launch stream; wall per call beside"}
+    if shard_ms:
+        line["shard_ms"] = shard_ms
+        line["shard_balance"] = max(shard_ms) / (sum(shard_ms) / len(shard_ms))
+        line["shard_sizes"] = np.diff(bounds).tolist()
     try:
         pmc = json.load(open(os.path.join(ROOT, C5_PMC_FILE)))["c5_share"]
     except (OSError, ValueError, KeyError):

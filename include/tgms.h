@@ -33,11 +33,14 @@
  *   - HIP-graph capture: uniform solves (tgms_solve_uniform_device, any method, and
  *     tgms_solve_batch_device / tgms_refine_*_device on a uniform batch) may be
  *     captured into a caller's graph.  Inside a capture the scratch event handshake
- *     is skipped, so a graph holding band-KKT launches must be replayed in stream
- *     order with the handle's other band calls.  Calls that upload a host-side launch
- *     plan or grow scratch at call time (ragged batches, tgms_refine_loop_device,
- *     the multi-GPU calls, a band slab that must grow) return TGMS_ERR_UNSUPPORTED
- *     while their stream is capturing;
+ *     is skipped.  A band-KKT capture needs the handle's slab sized by an earlier
+ *     uncaptured band call of at least that M; from then on that slab belongs to
+ *     graphs (uncaptured calls get a slab of their own and never free a graph's), so
+ *     replays may run beside uncaptured calls, but graphs holding band launches of one
+ *     handle must be replayed in stream order with each other.  Calls that upload a
+ *     host-side launch plan or grow scratch at call time (ragged batches,
+ *     tgms_refine_loop_device, the multi-GPU calls, a band capture with no slab large
+ *     enough) return TGMS_ERR_UNSUPPORTED while their stream is capturing;
  *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
  *     TGMS_ERR_NO_DEVICE.
  *
@@ -196,6 +199,40 @@ int tgms_device_count(const tgms_handle* h); /* 1 for a tgms_create handle */
  * ~equal cost (reduced / band: 2 + M_b, dense KKT: (14 M_b + 2)^3 per trajectory). */
 tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t parts, int method,
                              int32_t* bounds);
+/* Host-only introspection of the multi-GPU schedule (no device, no RCCL needed): what a
+ * tgms_solve_batch_multi_device / tgms_refine_loop_multi_device call over device_count
+ * devices would do with this batch -- the shard bounds [device_count+1], every device's
+ * piece-workspace size (ws_bytes [device_count], nullable), the pieces (trajectory /
+ * segment ranges and the byte offsets of their arrays in the workspace) and every
+ * point-to-point transfer in issue order: scatter groups 0..3 (piece k's inputs of every
+ * device, device 0 -> dev), then gather groups 4..7 (piece k's results, dev -> device 0);
+ * each transfer is one ncclSend on one side and one ncclRecv on the other.  flags:
+ * TGMS_SCHED_* below.  Returns TGMS_ERR_INVALID_ARG (with *n_pieces / *n_xfers set to the
+ * sizes needed) when piece_cap or xfer_cap is too small. */
+#define TGMS_SCHED_REFINE 1
+#define TGMS_SCHED_END_DERIVS 2
+#define TGMS_SCHED_COEFFS 4
+#define TGMS_SCHED_STATUS 8
+#define TGMS_SCHED_COST 16
+#define TGMS_SCHED_SELF_GATHER 32 /* device 0's shard through the pipeline too (TGMS_MULTI_SELF_GATHER=1) */
+typedef struct tgms_piece {
+    int32_t dev, piece, lo, hi; /* trajectories [lo, hi) */
+    int64_t s0, s1;             /* segments [s0, s1) */
+    int64_t ws_off[9];          /* byte offsets: rebased seg_offsets, permutation, W, T, T2, ED, C, status, cost */
+} tgms_piece;
+typedef struct tgms_xfer {
+    int32_t dev, piece, gather; /* gather 0: device 0 -> dev (scatter), 1: dev -> device 0 */
+    int32_t array;              /* 0 W, 1 T, 2 end derivs, 3 coeffs, 4 status, 5 cost */
+    int64_t batch_elem;         /* element offset in the device-0 batch array */
+    int64_t ws_byte;            /* byte offset in dev's piece workspace */
+    int64_t count;              /* elements */
+    int32_t elem_bytes;         /* 8 (fp64) or 4 (int32) */
+    int32_t group;              /* RCCL group (ncclGroupStart .. ncclGroupEnd) in issue order */
+} tgms_xfer;
+tgms_status tgms_multi_schedule(int32_t device_count, int32_t B, const int32_t* seg_offsets, int method,
+                                int32_t flags, int32_t* bounds, int64_t* ws_bytes, tgms_piece* pieces,
+                                int32_t piece_cap, int32_t* n_pieces, tgms_xfer* xfers, int32_t xfer_cap,
+                                int32_t* n_xfers);
 /* Host pointers, blocking: upload to device 0, the multi-GPU solve, one download. */
 tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* seg_offsets,
                                    const double* waypoints, const double* seg_times,

@@ -81,3 +81,48 @@ def test_ragged_and_loop_calls_refuse_capture(solver):
     torch.cuda.synchronize()
     Ch, _, worst = solver.solve(so, W, T)
     assert worst == 0 and np.array_equal(C.cpu().numpy(), Ch)
+
+
+def test_band_graph_keeps_its_slab_when_the_handle_grows():
+    """a captured band-KKT launch bakes in the slab pointer.  Once a capture
+    has used a slab it belongs to graphs: an uncaptured call that needs a bigger slab
+    allocates its own (the graph's is never freed under it), and an uncaptured call
+    running beside a replay uses a different slab.  Capture, grow, replay (also
+    concurrently with uncaptured calls on another stream): every result exact."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver
+    B = 4096
+    data = {}
+    for M in (3, 16):
+        _, W, T = S.uniform_batch(B, M, seed=92 + M)
+        data[M] = (torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda())
+    with Solver(0) as s:
+        ref = {}
+        for M in (3, 16):  # the reduced solve as the reference
+            ref[M] = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+            s.solve_uniform_device(B, M, *data[M], ref[M])
+        s.set_method(METHOD_BAND_KKT)
+        out3 = torch.empty_like(ref[3])
+        s.solve_uniform_device(B, 3, *data[3], out3)  # slab for M = 3
+        torch.cuda.synchronize()
+        g, err = _capture(lambda st: s.solve_uniform_device(B, 3, *data[3], out3, stream=st))
+        assert err is None, err
+        out16 = torch.empty_like(ref[16])
+        s.solve_uniform_device(B, 16, *data[16], out16)  # grows: a new slab, the graph's stays
+        torch.cuda.synchronize()
+        tol = lambda a, b: float(((a - b).abs().amax(dim=(1, 3)) / b.abs().amax(dim=(1, 3))).max())
+        assert tol(out16, ref[16]) <= 1e-9
+        other = torch.cuda.Stream()
+        for _ in range(3):
+            out3.fill_(float("nan"))
+            out16.fill_(float("nan"))
+            g.replay()  # on the current stream
+            with torch.cuda.stream(other):  # beside it, uncaptured, on the handle's own slab
+                s.solve_uniform_device(B, 16, *data[16], out16, stream=other.cuda_stream)
+            torch.cuda.synchronize()
+            assert tol(out3, ref[3]) <= 1e-9
+            assert tol(out16, ref[16]) <= 1e-9
+        del g
+        s.set_method(METHOD_REDUCED)

@@ -88,3 +88,18 @@ def test_plan_shards_uniform_fast_path(lib, method):
             got = plan_shards(so, parts, method)
             ref = SH.ragged_bounds(so, parts, method if method == 1 else 0)
             np.testing.assert_array_equal(got, ref.astype(np.int32), err_msg=f"B={B} M={M} parts={parts}")
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_plan_shards_uniform_beyond_2_53(lib, method):
+    """A uniform batch whose total cost passes 2^53 (the dense cost at a huge M): the
+    running sum rounds in fp64, so the closed-form fast path would cut elsewhere; the
+    planner then takes the general prefix-sum rule and still matches shard.ragged_bounds
+    (ADVICE r03)."""
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd.solver import plan_shards
+    M = 1 << 20
+    so = (np.arange(1001, dtype=np.int64) * M).astype(np.int32)
+    assert 1000 * float(14 * M + 2) ** 3 > 2.0 ** 53 or method == 0
+    for parts in (2, 3, 7, 8):
+        np.testing.assert_array_equal(plan_shards(so, parts, method), SH.ragged_bounds(so, parts, method).astype(np.int32))

@@ -26,8 +26,23 @@ EXPORTS = [
     "tgms_sample_count", "tgms_sample_offsets", "tgms_sample_batch", "tgms_sample_batch_device",
     "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_loop_device", "tgms_refine_batch",
     "tgms_create_multi", "tgms_device_count", "tgms_plan_shards", "tgms_solve_batch_multi",
-    "tgms_solve_batch_multi_device", "tgms_refine_loop_multi_device",
+    "tgms_solve_batch_multi_device", "tgms_refine_loop_multi_device", "tgms_multi_schedule",
 ]
+
+SCHED_REFINE, SCHED_END_DERIVS, SCHED_COEFFS, SCHED_STATUS, SCHED_COST, SCHED_SELF_GATHER = 1, 2, 4, 8, 16, 32
+
+
+class Piece(ctypes.Structure):
+    """tgms_piece (include/tgms.h): one piece of one device's shard."""
+    _fields_ = [("dev", ctypes.c_int32), ("piece", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
+                ("s0", ctypes.c_int64), ("s1", ctypes.c_int64), ("ws_off", ctypes.c_int64 * 9)]
+
+
+class Xfer(ctypes.Structure):
+    """tgms_xfer (include/tgms.h): one ncclSend/ncclRecv pair of the multi-GPU schedule."""
+    _fields_ = [("dev", ctypes.c_int32), ("piece", ctypes.c_int32), ("gather", ctypes.c_int32),
+                ("array", ctypes.c_int32), ("batch_elem", ctypes.c_int64), ("ws_byte", ctypes.c_int64),
+                ("count", ctypes.c_int64), ("elem_bytes", ctypes.c_int32), ("group", ctypes.c_int32)]
 
 _lib = None
 
@@ -101,6 +116,8 @@ def load(path: str = ""):
     L.tgms_solve_batch_multi_device.restype = ctypes.c_int
     L.tgms_refine_loop_multi_device.argtypes = [vp, i32, vp, vp, vp, vp, vp, dbl, dbl, i32, vp, vp, vp, vp]
     L.tgms_refine_loop_multi_device.restype = ctypes.c_int
+    L.tgms_multi_schedule.argtypes = [i32, i32, vp, ctypes.c_int, i32, vp, vp, vp, i32, vp, vp, i32, vp]
+    L.tgms_multi_schedule.restype = ctypes.c_int
     if L.tgms_abi_version() != ABI_VERSION:
         raise ImportError(f"libtgms ABI {L.tgms_abi_version()} != {ABI_VERSION}")
     _lib = L

@@ -26,6 +26,7 @@ ARCH = os.environ.get("TGMS_ARCH", "gfx950")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 
 HIP_SOURCES = ["tgms_reduced.hip", "tgms_dense.hip", "tgms_band.hip", "tgms_sample.hip", "tgms_capi.hip"]
+CXX_SOURCES = ["tgms_plan.cpp"]  # host-only (no HIP): compiled by g++ into the same library
 HOST_SOURCES = ["MinSnap.cpp", "factory.cpp", "tgms_node_capi.cpp"]
 
 
@@ -57,8 +58,17 @@ def build_tgms(force: bool = False) -> str:
     objs = [os.path.join(OBJDIR, os.path.basename(s) + ".o") for s in srcs]
     hdrs = _headers()
     todo = [(s, o) for s, o in zip(srcs, objs) if force or _newer(o, [s] + hdrs)]
-    with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
-        list(ex.map(lambda so: _run([HIPCC] + HIP_FLAGS + ["-c", so[0], "-o", so[1]]), todo))
+    csrcs = [os.path.join(CSRC, s) for s in CXX_SOURCES]
+    cobjs = [os.path.join(OBJDIR, os.path.basename(s) + ".o") for s in csrcs]
+    ctodo = [(s, o) for s, o in zip(csrcs, cobjs) if force or _newer(o, [s] + hdrs)]
+    cxx = ["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-I" + INCLUDE, "-I" + CSRC]
+    with ThreadPoolExecutor(max_workers=len(srcs) + len(csrcs)) as ex:
+        jobs = [ex.submit(_run, [HIPCC] + HIP_FLAGS + ["-c", s, "-o", o]) for s, o in todo]
+        jobs += [ex.submit(_run, cxx + ["-c", s, "-o", o]) for s, o in ctodo]
+        for j in jobs:
+            j.result()
+    objs = objs + cobjs
+    todo = todo + ctodo
     if force or todo or _newer(LIB_TGMS, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB_TGMS] + objs + ["-ldl"])
     return LIB_TGMS

@@ -522,7 +522,11 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         // this wave stored are read back by other lanes of the wave: wait for the stores to
         // reach L2 and read them with L1-bypassing loads (the slab is reused by the next
         // group, so L1 may hold the previous one's lines)
+#ifdef TGMS_BAND_FENCE  // diagnosis build: a full agent-scope acquire/release at the hand-off
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         constexpr int kN = N - 1;
         const int lb = opaque(lane % BL);
 #pragma unroll 1
@@ -563,9 +567,18 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
                 if (!valid) st = TGMS_ERR_INVALID_ARG;
                 else if (singular) st = TGMS_ERR_SINGULAR;
                 else if (nonfinite) st = TGMS_ERR_NONFINITE;
+#ifdef TGMS_BAND_HWID  // diagnosis build (scripts/band_hwdiag.py): where the trajectory ran
+                uint32_t hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                st = (int32_t)((hw & 0x000FFFFFu) | ((xcc & 0xFu) << 20) | ((uint32_t)(st & 0xF) << 24));
+#endif
                 status[bb] = st;
             }
         }
+#ifdef TGMS_BAND_FENCE
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+#endif
         asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }

@@ -37,7 +37,10 @@ hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nul
 // of `grid` wavefronts, each with private U slabs in `scratch` (band_scratch_bytes).
 // grid = CUs x BAND_WAVES_PER_CU (the scratch is sized for it: one wavefront per SIMD,
 // the register budget of the kernel); the launch uses the resident part of it.
-constexpr int BAND_WAVES_PER_CU = 4;
+#ifndef TGMS_BAND_WAVES_PER_CU
+#define TGMS_BAND_WAVES_PER_CU 4
+#endif
+constexpr int BAND_WAVES_PER_CU = TGMS_BAND_WAVES_PER_CU;
 size_t band_scratch_bytes(int M, int32_t grid);
 hipError_t launch_band_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nullable*/,
                            const int32_t* seg_offsets /*nullable if uniform*/, const double* W,

@@ -251,3 +251,30 @@ def plan_shards(seg_offsets, parts: int, method: int = _lib.METHOD_REDUCED) -> n
     if st != _lib.OK:
         raise TgmsError(st, "tgms_plan_shards")
     return bounds
+
+
+def multi_schedule(seg_offsets, device_count: int, method: int = _lib.METHOD_REDUCED, flags: int = 0):
+    """tgms_multi_schedule (host only): the multi-GPU call's whole schedule -- shard bounds,
+    per-device workspace sizes, pieces and transfers (lists of dicts, issue order)."""
+    import ctypes
+    L = _lib.load()
+    so = np.ascontiguousarray(seg_offsets, dtype=np.int32)
+    B = int(so.shape[0] - 1)
+    n = int(device_count)
+    bounds = np.zeros(n + 1, dtype=np.int32)
+    ws = np.zeros(n, dtype=np.int64)
+    npc, nx = ctypes.c_int32(0), ctypes.c_int32(0)
+    st = L.tgms_multi_schedule(n, B, _ptr(so), int(method), int(flags), _ptr(bounds), _ptr(ws), None, 0,
+                               ctypes.byref(npc), None, 0, ctypes.byref(nx))
+    if st not in (_lib.OK, _lib.ERR_INVALID_ARG) or (st != _lib.OK and npc.value == 0 and nx.value == 0):
+        raise TgmsError(st, "tgms_multi_schedule")
+    pieces = (_lib.Piece * max(1, npc.value))()
+    xfers = (_lib.Xfer * max(1, nx.value))()
+    st = L.tgms_multi_schedule(n, B, _ptr(so), int(method), int(flags), _ptr(bounds), _ptr(ws), pieces, npc.value,
+                               ctypes.byref(npc), xfers, nx.value, ctypes.byref(nx))
+    if st != _lib.OK:
+        raise TgmsError(st, "tgms_multi_schedule")
+    P = [{"dev": p.dev, "piece": p.piece, "lo": p.lo, "hi": p.hi, "s0": p.s0, "s1": p.s1,
+          "ws_off": list(p.ws_off)} for p in pieces[: npc.value]]
+    X = [{f: getattr(x, f) for f, _ in _lib.Xfer._fields_} for x in xfers[: nx.value]]
+    return bounds, ws, P, X
