@@ -153,6 +153,7 @@ def cpu_baseline(B: int, M: int, target_s: float):
 
 
 C5_PMC_FILE = "profiles/c5_pmc.json"
+BYTE_MIX_FLOOR_US = 28.6  # config 3's byte mix with no compute, best occupancy (profiles/r03_runstore_occ.txt)
 
 
 def _c5_shard(so_all, W_all, T_all, bounds, part, dev):
@@ -1012,6 +1013,14 @@ def main():
                          "kernel": (f"k_dense_kkt<{M}>" if args.method == "dense" else
                                     f"k_lane_uniform<{M}>" if M % 2 == 0 else f"k_reduced_uniform<{M}>"),
                          "launch_ms": launch_ms_max,
+                         # the measured floor of this byte mix with NO compute (read the inputs,
+                         # write the coefficients, fresh buffers, best occupancy and rounds:
+                         # scripts/micro/occstore.hip, profiles/r03_runstore_occ.txt): the
+                         # fraction of the attainable rate the kernel reaches
+                         "floor_us": BYTE_MIX_FLOOR_US if (B, M) == (65536, 10) else None,
+                         "floor_frac": (BYTE_MIX_FLOOR_US / (launch_ms_max * 1e3)) if (B, M) == (65536, 10) else None,
+                         "floor_source": "profiles/r03_runstore_occ.txt (reads + stores, no compute, 2 waves/SIMD, "
+                                         "4 rounds: 28.6 us for 22.5 MB read + 126 MB written)",
                          "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
                          "algorithmic_bytes_per_launch": bpl},
             "cpu_baseline": cpu,

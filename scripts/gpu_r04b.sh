@@ -23,6 +23,6 @@ for lib in default $V/libtgms_v2c8.so; do
 done
 done
 cut -c1-150 $OUT/band_b.jsonl
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_multi.py tests/test_gpu_capture.py > $OUT/pytest_b.log 2>&1; c=$?
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_multi.py tests/test_gpu_capture.py tests/test_gpu_edges.py > $OUT/pytest_b.log 2>&1; c=$?
 echo "pytest exit $c"; tail -3 $OUT/pytest_b.log
 exit $c

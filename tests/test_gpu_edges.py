@@ -123,6 +123,38 @@ def test_breakdown_writes_exact_zeros(solver, method, t_small):
     _, st, worst = solver.solve(so, W, T, out=(C, st))
     assert st[0] == OK and st[2] == OK
     assert st[1] in (OK, ERR_SINGULAR, ERR_NONFINITE)
-    if st[1] == ERR_SINGULAR:
+    if st[1] in (ERR_SINGULAR, ERR_NONFINITE):  # every failure status: exact zeros
         assert (C[2:4] == 0.0).all(), C[2:4]
     assert np.isfinite(C[[0, 1, 4, 5]]).all()
+
+
+@pytest.mark.parametrize("M", [2, 3, 10])
+def test_overflow_reports_nonfinite_and_writes_zeros(solver, method, M):
+    """Finite inputs whose solution overflows (waypoints near DBL_MAX): the trajectory is
+    reported TGMS_ERR_NONFINITE and comes out as exact zeros, like every other failure
+    (the emit gate used to cover only invalid and singular trajectories); its
+    neighbours are unaffected.  Even M goes through the lane kernel (uniform, reduced),
+    odd M through the lane-pair kernel, every method through its own kernel; the ragged
+    form covers the grouped paths."""
+    from trajectory_generator_ros2_amd import ERR_NONFINITE, OK
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(5, M, seed=78 + M)
+    W, T = W.reshape(-1, 3).copy(), T.reshape(-1)
+    W[2 * (M + 1): 3 * (M + 1)] *= 1e306  # trajectory 2: every waypoint near the top of the range
+    assert np.isfinite(W).all()
+    for ragged in (False, True):
+        so_r = so
+        W_r, T_r = W, T
+        if ragged:  # append a 1-segment trajectory: the batch is no longer uniform
+            so_r = np.concatenate([so, [so[-1] + 1]]).astype(np.int32)
+            W_r = np.concatenate([W, [[0, 0, 1], [1, 1, 1]]])
+            T_r = np.concatenate([T, [1.0]])
+        C = np.full((int(so_r[-1]), 3, 8), np.nan)
+        st = np.full(len(so_r) - 1, -1, np.int32)
+        _, st, _ = solver.solve(so_r, W_r, T_r, out=(C, st))
+        assert st[2] == ERR_NONFINITE, (ragged, st)
+        assert (C[2 * M: 3 * M] == 0.0).all(), C[2 * M: 3 * M]
+        others = [b for b in range(len(so_r) - 1) if b != 2]
+        assert (st[others] == OK).all(), st
+        for b in others:
+            assert np.isfinite(C[so_r[b]: so_r[b + 1]]).all()

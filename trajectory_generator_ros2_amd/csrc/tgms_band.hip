@@ -575,6 +575,14 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
 #endif
                 status[bb] = st;
             }
+            // a non-finite solution is rewritten as exact zeros, like every other failure
+            // (its coefficients were stored during the sweep): rare path, after this
+            // wave's own stores to the range have completed
+            if (liveq && valid && !singular && nonfinite) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int64_t mq = seg_offsets ? (int64_t)seg_offsets[bb + 1] - sq : M;
+                for (int64_t e = lb; e < mq * 24; e += BL) out[e] = 0.0;
+            }
         }
 #ifdef TGMS_BAND_FENCE
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");

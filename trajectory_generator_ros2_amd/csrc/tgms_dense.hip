@@ -304,6 +304,10 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     // status: any non-finite coefficient anywhere in the workgroup
     if (!(fin * 0.0 == 0.0)) atomicOr(&s_bad, 2);
     __syncthreads();
+    // a non-finite solution is rewritten as exact zeros, like every other failure (the
+    // barrier above waited for every thread's coefficient stores)
+    if ((s_bad & 2) && valid && !singular)
+        for (int e = tid; e < 24 * M; e += GJ_T) C[s0 * 24 + e] = 0.0;
     if (tid == 0 && status) {
         int32_t st = TGMS_OK;
         if (!valid) st = TGMS_ERR_INVALID_ARG;

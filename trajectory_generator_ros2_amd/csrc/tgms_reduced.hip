@@ -763,6 +763,15 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
     return TGMS_OK;
 }
 
+// A trajectory whose solution came out non-finite is rewritten as exact zeros, like every
+// other failure (its coefficients were already stored during the solve).  Rare path: the
+// wave first waits for its own stores to the range, then lanes first, first + step, ...
+// rewrite it.
+__device__ __forceinline__ void zero_traj(double* c, int n, int first, int step) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int e = first; e < n; e += step) c[e] = 0.0;
+}
+
 // Anchor a value at this point of the instruction stream: it must be computed before
 // the (volatile, ordered) statement, so IR-level sinking cannot pile every step's
 // arithmetic into one block after the last scheduling fence (which only orders the
@@ -1180,6 +1189,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
     const int32_t st = pair_solve<M, HAS_ED, OutBuf>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
     STAMP(5);
     STAMP_RT(7);
+    if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + b * (M * 24), M * 24, right, 2);
     if (live && !right && status) status[b] = st;
 }
 
@@ -1338,6 +1348,7 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
     const LaneView L = make_view<M>(sm.in, slot, right);
     const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
     const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, O);
+    if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + sm.in.base[slot], M * 24, right, 2);
     if (live && !right && status) status[b] = st;
 }
 
@@ -1434,6 +1445,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         const LaneView L = make_view<M>(sm.in, slot, right);
         const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
         const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, ed, O);
+        if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + sm.in.base[slot], M * 24, right, 2);
         if (live && !right && status) status[b] = st;
     } else if (live && !right && status) {
         status[b] = st_last;
@@ -2064,6 +2076,7 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
         st = TGMS_ERR_SINGULAR;
     else if (!finite(fin))
         st = TGMS_ERR_NONFINITE;
+    if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + b * (M * 24), M * 24, 0, 1);
     if (live && status) status[b] = st;
 }
 
