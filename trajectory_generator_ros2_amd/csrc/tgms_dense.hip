@@ -7,6 +7,8 @@
 // 256-thread workgroup (k_dense_gj below).  Round 1's kernel kept the matrix in LDS
 // (161 KB at M = 10: one trajectory per CU) and was bound by dependent LDS round trips
 // (122 ms per 65,536); this one holds two trajectories per CU in registers (45 ms).
+#include <type_traits>
+
 #include "tgms_device.h"
 #include "tgms_internal.h"
 
@@ -317,15 +319,317 @@ __global__ __launch_bounds__(GJ_T, 2) void k_dense_gj(int32_t n_traj, const int3
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two columns per barrier pair (round 4).  The same Gauss-Jordan
+// elimination, bit for bit (the same pivots, the same fma sequence per entry), with the
+// columns taken in pairs (k, k+1) (N = 14M+2 is even):
+//   lookahead (one wave: the one owning column groups k % 16 and k % 16 + 1, which are
+//   two 16-lane rows of it since k is even): the pivot p_k of column k and its multipliers
+//   l_k; column k+1 after step k, c' = fma(-l_k, a[p_k][k+1], c) (a[p_k][k+1] read from the
+//   owner lane by readlane); the pivot p_{k+1} of c' over the rows still active without
+//   p_k, and the multipliers l_{k+1} = c' / c'[p_{k+1}] (0 for p_{k+1});      barrier A
+//   pivot rows: row p_k's owners publish u_k = row p_k; row p_{k+1}'s owners publish
+//   u'_{k+1} = fma(-l_k[p_{k+1}], u_k, row p_{k+1}) (u_k read back from LDS inside the
+//   wave: the same column group is one 16-lane row of one wave);            barrier B
+//   rank-2 update: a = fma(-l_{k+1}, u'_{k+1}, fma(-l_k, u_k, a)), then the next pair's
+//   lookahead.
+// Two workgroup barriers per two columns instead of per column; the multipliers and the
+// pivot record are double-buffered (the next pair's lookahead writes them while slower
+// waves still update with the current ones).
+#ifndef TGMS_DENSE_PANEL
+#define TGMS_DENSE_PANEL 0  // 1 after GPU validation (scripts/dense_ab.py)
+#endif
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(GJ_T, 2) void k_dense_gj2(int32_t n_traj, const int32_t* __restrict__ ids,
+                                                       const int32_t* __restrict__ seg_offsets,
+                                                       const double* __restrict__ W, const double* __restrict__ T,
+                                                       const double* __restrict__ ED, double* __restrict__ C,
+                                                       int32_t* __restrict__ status) {
+    using S = GJShape<M>;
+    constexpr int n = S::n, N = S::N, RI = S::RI, CJ = S::CJ;
+    static_assert(N % 2 == 0, "columns are eliminated in pairs");
+    static_assert(GJ_G == 16 && GJ_C == 16, "a column group is one DPP row; four per wave");
+    __shared__ double s_pw[M][8];
+    __shared__ double s_w[(M + 1) * 3];
+    __shared__ double s_ed[18];
+    constexpr int US = CJ, LS = (RI + 1) & ~1;
+    __shared__ double s_u[2][GJ_C * US];          // u_k, u'_{k+1} (columns <= k+1 stale: never read again)
+    __shared__ alignas(16) double s_l[2][2][GJ_G * LS];  // [pair parity][column of the pair][multipliers]
+    __shared__ double s_pd[2][2];                 // [parity][column]: signed pivot
+    __shared__ int s_pr[2][2];                    // [parity][column]: pivot row
+    __shared__ double s_ipiv[N];
+    __shared__ int s_rowpos[N];  // elimination position of each row (N: never pivoted)
+    __shared__ int s_bad;
+
+    const int tid = threadIdx.x;
+    const int tr = tid % GJ_G, tc = tid / GJ_G;
+    const int32_t bi = blockIdx.x;
+    const int32_t b = ids ? ids[bi] : bi;
+    const int64_t s0 = seg_offsets ? (int64_t)seg_offsets[b] : (int64_t)b * M;
+
+    // ---- inputs (validated; an invalid trajectory is solved with unit times, zero
+    // waypoints and end derivatives and comes out as zeros) ----
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    {
+        int bad = 0;
+        if (tid < M) {
+            const double t = T[s0 + tid];
+            bad |= !finite_pos(t);
+            double p = 1.0;
+            for (int e = 0; e < 8; ++e) {
+                s_pw[tid][e] = p;
+                p *= t;
+            }
+        }
+        if (tid < (M + 1) * 3) {
+            const double v = W[(s0 + b) * 3 + tid];
+            bad |= !finite(v);
+            s_w[tid] = v;
+        }
+        if (HAS_ED && tid < 18) {
+            const double v = ED[(int64_t)b * 18 + tid];
+            bad |= !finite(v);
+            s_ed[tid] = v;
+        }
+        if (bad) atomicOr(&s_bad, 1);
+    }
+    __syncthreads();
+    const bool valid = s_bad == 0;
+    if (!valid) {
+        if (tid < M)
+            for (int e = 0; e < 8; ++e) s_pw[tid][e] = 1.0;
+        if (tid < (M + 1) * 3) s_w[tid] = 0.0;
+        if (tid < 18) s_ed[tid] = 0.0;
+        __syncthreads();
+    }
+
+    double a[RI][CJ];
+#pragma unroll
+    for (int i = 0; i < RI; ++i)
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) a[i][j] = gj_entry<M, HAS_ED>(tr + GJ_G * i, tc + GJ_C * j, s_pw, s_w, s_ed);
+    unsigned act = 0;  // rows not yet pivoted (bit i: row tr + 16 i)
+#pragma unroll
+    for (int i = 0; i < RI; ++i) act |= (tr + GJ_G * i < N) ? (1u << i) : 0u;
+    for (int r = tid; r < N; r += GJ_T) s_rowpos[r] = N;  // (ordered by the first barrier below)
+
+    // the largest |v_i| over the rows in `msk`, ties to the lowest row, reduced over the
+    // 16-lane row by DPP (every lane ends with the row's result)
+    auto pick = [&](auto get, unsigned msk, double& sv, int& brow) {
+        sv = 0.0;
+        brow = N;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) {
+            const double vi = get(i);
+            const bool take = ((msk >> i) & 1u) && fabs(vi) > fabs(sv);
+            sv = take ? vi : sv;
+            brow = take ? tr + GJ_G * i : brow;
+        }
+        auto merge = [&](double osv, int orow) {
+            const bool take = (fabs(osv) > fabs(sv)) || (fabs(osv) == fabs(sv) && orow < brow);
+            sv = take ? osv : sv;
+            brow = take ? orow : brow;
+        };
+        merge(dpp_f64<0xB1>(sv), __builtin_amdgcn_mov_dpp(brow, 0xB1, 0xF, 0xF, false));
+        merge(dpp_f64<0x4E>(sv), __builtin_amdgcn_mov_dpp(brow, 0x4E, 0xF, 0xF, false));
+        merge(dpp_f64<0x141>(sv), __builtin_amdgcn_mov_dpp(brow, 0x141, 0xF, 0xF, false));
+        merge(dpp_f64<0x140>(sv), __builtin_amdgcn_mov_dpp(brow, 0x140, 0xF, 0xF, false));
+    };
+
+    // lookahead of pair (k, k+1), k even: run by the wave holding column groups kg, kg+1.
+    // Both columns sit in register column j0 = k / 16 of their owners; the body is
+    // instantiated per j0 (a uniform branch) so it works on a[i][j0] in place.
+    auto lookahead_j = [&](auto J, int k, int par) {
+        constexpr int j0 = decltype(J)::value;
+        const int kg = k % GJ_C;
+        const bool own0 = tc == kg, own1 = tc == kg + 1;
+        double sv0 = 0.0;
+        int br0 = N;
+        if (own0) pick([&](int i) { return a[i][j0]; }, act, sv0, br0);
+        const int l0 = GJ_G * (kg & 3);
+        const double ps0 = readlane_f64(sv0, l0);
+        const int p0 = __builtin_amdgcn_readlane(br0, l0);
+        const double ip0 = fast_rcp(ps0);
+        const int pg0 = p0 % GJ_G, pi0 = p0 / GJ_G;
+        if (own0) {
+#pragma unroll
+            for (int i = 0; i < RI; ++i) s_l[par][0][tr * LS + i] = (tr + GJ_G * i == p0) ? 0.0 : a[i][j0] * ip0;
+            if (tr == 0) {
+                s_pd[par][0] = ps0;
+                s_pr[par][0] = p0;
+            }
+        }
+        // a[p_k][k+1]: lane (row kg+1, tr = pg0), register (pi0, j0)
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) v = (i == pi0) ? a[i][j0] : v;
+        const double uk1 = readlane_f64(v, GJ_G * ((kg + 1) & 3) + pg0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // l_k written (this wave's own LDS order)
+        __builtin_amdgcn_wave_barrier();
+        if (own1) {
+            // column k+1 after step k, in place: the column is dead once the pair is done
+            // (the rank-2 update's second touch of it, and u'_{k+1}[k+1], are never read)
+#pragma unroll
+            for (int i = 0; i < RI; ++i) a[i][j0] = __builtin_fma(-s_l[par][0][tr * LS + i], uk1, a[i][j0]);
+            const unsigned msk = act & ~((tr == pg0) ? (1u << pi0) : 0u);
+            double sv1;
+            int br1;
+            pick([&](int i) { return a[i][j0]; }, msk, sv1, br1);
+            const double ip1 = fast_rcp(sv1);
+#pragma unroll
+            for (int i = 0; i < RI; ++i) s_l[par][1][tr * LS + i] = (tr + GJ_G * i == br1) ? 0.0 : a[i][j0] * ip1;
+            if (tr == 0) {
+                s_pd[par][1] = sv1;
+                s_pr[par][1] = br1;
+            }
+        }
+    };
+    auto lookahead = [&](int k, int par) {
+        if ((tc >> 2) != ((k % GJ_C) >> 2)) return;  // wave-uniform: only the owner wave
+        const int j0 = k / GJ_C;
+#define TGMS_LA(jj) \
+    if constexpr (jj < CJ) if (j0 == jj) lookahead_j(std::integral_constant<int, jj>{}, k, par);
+        TGMS_LA(0) TGMS_LA(1) TGMS_LA(2) TGMS_LA(3) TGMS_LA(4) TGMS_LA(5) TGMS_LA(6) TGMS_LA(7) TGMS_LA(8)
+        TGMS_LA(9) TGMS_LA(10) TGMS_LA(11) TGMS_LA(12) TGMS_LA(13) TGMS_LA(14) TGMS_LA(15)
+#undef TGMS_LA
+    };
+
+    lookahead(0, 0);
+    __syncthreads();
+
+    bool singular = false;
+    for (int k = 0; k < N; k += 2) {
+        const int par = (k >> 1) & 1;
+        // ---- the pair's pivots (found by the lookahead) ----
+        const double ps0 = s_pd[par][0], ps1 = s_pd[par][1];
+        const int p0 = __builtin_amdgcn_readfirstlane(s_pr[par][0]);
+        const int p1 = __builtin_amdgcn_readfirstlane(s_pr[par][1]);
+        if (!(fabs(ps0) > 0.0) || !(fabs(ps1) > 0.0)) {  // identical in every thread
+            singular = true;
+            break;
+        }
+        if (tid == 0) {
+            s_ipiv[k] = fast_rcp(ps0);
+            s_ipiv[k + 1] = fast_rcp(ps1);
+            s_rowpos[p0] = k;
+            s_rowpos[p1] = k + 1;
+        }
+        const int pg0 = p0 % GJ_G, pi0 = p0 / GJ_G, pg1 = p1 % GJ_G, pi1 = p1 / GJ_G;
+        // ---- pivot rows: u_k, then u'_{k+1} from it (the same column group: one wave) ----
+        if (tr == pg0) {
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                if (i == pi0) {
+#pragma unroll
+                    for (int j = 0; j < CJ; ++j) s_u[0][tc * US + j] = a[i][j];
+                }
+            }
+            act &= ~(1u << pi0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (tr == pg1) {
+            const double lp = s_l[par][0][pg1 * LS + pi1];
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                if (i == pi1) {
+#pragma unroll
+                    for (int j = 0; j < CJ; ++j) s_u[1][tc * US + j] = __builtin_fma(-lp, s_u[0][tc * US + j], a[i][j]);
+                }
+            }
+            act &= ~(1u << pi1);
+        }
+        __syncthreads();
+        // ---- rank-2 update (column blocks left of k are done), in two halves of the
+        // thread's rows so only half of the multipliers are live at a time ----
+        constexpr int RH = (RI + 1) / 2;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            double la[RH], lb[RH];
+#pragma unroll
+            for (int q = 0; q < RH; ++q) {
+                const int i = h * RH + q;
+                if (i < RI) {
+                    la[q] = s_l[par][0][tr * LS + i];
+                    lb[q] = s_l[par][1][tr * LS + i];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < CJ; ++j) {
+                if (GJ_C * j + GJ_C - 1 > k) {  // uniform
+                    const double u0 = s_u[0][tc * US + j], u1 = s_u[1][tc * US + j];
+#pragma unroll
+                    for (int q = 0; q < RH; ++q) {
+                        const int i = h * RH + q;
+                        if (i < RI) a[i][j] = __builtin_fma(-lb[q], u1, __builtin_fma(-la[q], u0, a[i][j]));
+                    }
+                }
+            }
+        }
+        if (k + 2 < N) lookahead(k + 2, par ^ 1);
+        __syncthreads();
+    }
+
+    // ---- x_k = b'_{p_k} / a_{p_k k} (as k_dense_gj) ----
+    if (singular) {
+        for (int e = tid; e < 24 * M; e += GJ_T) C[s0 * 24 + e] = 0.0;
+    }
+    double fin = 0.0;
+#pragma unroll
+    for (int j = 0; j < CJ; ++j) {
+        const int c = tc + GJ_C * j;
+        if (c >= N && c < N + 3) {
+            const int ax = c - N;
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const int r = tr + GJ_G * i;
+                const int k = r < N ? s_rowpos[r] : N;
+                if (k < n && !singular) {
+                    const double x = a[i][j] * s_ipiv[k];
+                    fin += x;
+                    C[s0 * 24 + ((k >> 3) * 3 + ax) * 8 + (k & 7)] = valid ? x : 0.0;
+                }
+            }
+        }
+    }
+    if (!(fin * 0.0 == 0.0)) atomicOr(&s_bad, 2);
+    __syncthreads();
+    if ((s_bad & 2) && valid && !singular)
+        for (int e = tid; e < 24 * M; e += GJ_T) C[s0 * 24 + e] = 0.0;
+    if (tid == 0 && status) {
+        int32_t st = TGMS_OK;
+        if (!valid) st = TGMS_ERR_INVALID_ARG;
+        else if (singular) st = TGMS_ERR_SINGULAR;
+        else if (s_bad & 2) st = TGMS_ERR_NONFINITE;
+        status[b] = st;
+    }
+}
+
 template <int M>
 hipError_t dense_M(int32_t n_traj, const int32_t* ids, const int32_t* so, const double* W,
                    const double* T, const double* ED, double* C, int32_t* status,
                    hipStream_t stream) {
     if (n_traj <= 0) return hipSuccess;
+#if TGMS_DENSE_PANEL
+    if (ED)
+        TGMS_LAUNCH((k_dense_gj2<M, true>), dim3(n_traj), dim3(GJ_T), 0, stream, n_traj, ids, so, W, T, ED, C, status);
+    else
+        TGMS_LAUNCH((k_dense_gj2<M, false>), dim3(n_traj), dim3(GJ_T), 0, stream, n_traj, ids, so, W, T, ED, C, status);
+#else
     if (ED)
         TGMS_LAUNCH((k_dense_gj<M, true>), dim3(n_traj), dim3(GJ_T), 0, stream, n_traj, ids, so, W, T, ED, C, status);
     else
         TGMS_LAUNCH((k_dense_gj<M, false>), dim3(n_traj), dim3(GJ_T), 0, stream, n_traj, ids, so, W, T, ED, C, status);
+#endif
     return hipSuccess;
 }
 
