@@ -27,3 +27,15 @@ for lib in b4 b4w2; do
   echo "pytest $lib exit $c"; tail -2 $OUT/pytest_d_$lib.log
   [ $c -eq 0 ] || exit $c
 done
+# uniform M = 12/14/16: the lane kernel (spills to scratch at these M) against the lane-pair
+# kernel (TGMS_LANE_MAX_M=10 variant), fresh batches
+for m in 12 14 16; do
+  for lib in default $V/libtgms_lanemax10.so; do
+    if [ $lib = default ]; then L=""; else L=$lib; fi
+    TGMS_LIB=$L KB_M=$m KB_ROT=3 KB_K=20 timeout -k 10 300 python3 scripts/kbench.py >> $OUT/lane_d.jsonl 2>> $OUT/lane_d.err || exit 1
+  done
+done
+cut -c1-200 $OUT/lane_d.jsonl
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_configs.py tests/test_gpu_edges.py tests/test_gpu_parity.py > $OUT/pytest_d_main.log 2>&1; c=$?
+echo "pytest main exit $c"; tail -2 $OUT/pytest_d_main.log
+exit $c

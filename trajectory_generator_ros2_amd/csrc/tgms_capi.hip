@@ -324,12 +324,13 @@ tgms_status run_chains(tgms_handle* h, hipStream_t stream,
 
 // Reduced method, ragged plan: every M group in one launch per occupancy class
 // (M <= 11 / M >= 12), the longest groups' wavefronts first.
-void class_tables(const Plan& p, tgms::GroupTable (&tab)[2]) {
+void class_tables(const Plan& p, bool has_ed, tgms::GroupTable (&tab)[2]) {
     tab[0] = tgms::GroupTable{};
     tab[1] = tgms::GroupTable{};
+    const int max2 = tgms::two_wave_max_m(has_ed);
     for (size_t m = p.counts.size(); m-- > 1;) {
         if (!p.counts[m]) continue;
-        tgms::GroupTable& t = tab[m > TGMS_TWO_WAVE_MAX_M ? 1 : 0];
+        tgms::GroupTable& t = tab[(int)m > max2 ? 1 : 0];
         const int g = t.ngroups++;
         t.m[g] = (int32_t)m;
         t.n[g] = p.counts[m];
@@ -342,7 +343,7 @@ tgms_status run_ragged_multi(tgms_handle* h, const Plan& p, hipStream_t stream, 
                              const double* W, const double* T, const double* ED, double kT, double eta,
                              double* Tout, double* cost, double* C, int32_t* st) {
     tgms::GroupTable tab[2];
-    class_tables(p, tab);
+    class_tables(p, ED != nullptr, tab);
     std::vector<std::function<hipError_t(hipStream_t)>> jobs;
     for (int c = 1; c >= 0; --c)
         if (tab[c].ngroups)
@@ -456,7 +457,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         // times kept in LDS between steps and updated in place in T[0]; the two classes'
         // launches run side by side.
         tgms::GroupTable tab[2];
-        class_tables(p, tab);
+        class_tables(p, ED != nullptr, tab);
         std::vector<std::function<hipError_t(hipStream_t)>> jobs;
         // the one-wave class first (launching the longer two-wave class first, or both
         // without the loop's graph, measured 0.58-0.60 ms against 0.52-0.53)
@@ -478,7 +479,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, const int32_t*
         // the end; neither waits for the other's step (each class alone fills ~2/3 of
         // the GPU).
         tgms::GroupTable tab[2];
-        class_tables(p, tab);
+        class_tables(p, ED != nullptr, tab);
         // one op list per class; ops are issued round-robin across the classes so a
         // captured graph holds them interleaved and launches both chains side by side
         // (capturing one whole chain first held the other back by its ~80 us of

@@ -11,6 +11,12 @@ namespace tgms {
 #ifndef TGMS_TWO_WAVE_MAX_M
 #define TGMS_TWO_WAVE_MAX_M 11
 #endif
+// ... and with end derivatives (their extra state spills the fused refinement loop at
+// M = 11 within 256 registers; M <= 10 fits with none)
+#ifndef TGMS_TWO_WAVE_MAX_M_ED
+#define TGMS_TWO_WAVE_MAX_M_ED 10
+#endif
+constexpr int two_wave_max_m(bool has_ed) { return has_ed ? TGMS_TWO_WAVE_MAX_M_ED : TGMS_TWO_WAVE_MAX_M; }
 
 // Reduced-Hessian solve, uniform M (configs 2-4).  Grid: ceil(B/64) waves.
 hipError_t launch_reduced_uniform(int M, int32_t B, const double* W, const double* T,
@@ -57,7 +63,8 @@ hipError_t launch_refine_ragged_group(int M, int32_t n, const int32_t* perm, con
 
 // Several M groups of a ragged batch in one launch.  Group g owns wavefronts
 // [blk_end[g-1], blk_end[g]) and its n[g] trajectories perm[g][0..n) have m[g] segments.
-// cls 0 takes M in 1..11 (two waves per SIMD), cls 1 M in 12..16 (one wave per SIMD).
+// cls 0 takes M in 1..two_wave_max_m(ED) (two waves per SIMD), cls 1 the larger M (one wave
+// per SIMD).
 constexpr int RAGGED_TPW = 32;  // trajectories per wavefront of the reduced kernels
 struct GroupTable {
     int32_t ngroups;

@@ -2084,9 +2084,14 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
 #ifndef TGMS_LANE_UNIFORM
 #define TGMS_LANE_UNIFORM 1
 #endif
+// Largest M on the lane kernel: its whole elimination state lives in registers, which
+// at M >= 12 spill to scratch (92-980 B per lane); those M take the lane-pair kernel.
+#ifndef TGMS_LANE_MAX_M
+#define TGMS_LANE_MAX_M 16
+#endif
 template <int M>
 constexpr bool use_lane_kernel() {
-    return TGMS_LANE_UNIFORM && M >= 2 && M % 2 == 0;
+    return TGMS_LANE_UNIFORM && M >= 2 && M % 2 == 0 && M <= TGMS_LANE_MAX_M;
 }
 
 template <int M>
@@ -2200,17 +2205,25 @@ hipError_t loop_multi_launch(const GroupTable& tab, const int32_t* so, const dou
 hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* so, const double* W, double* T,
                                     const double* ED, double kT, double eta, int32_t iters, double* cost, double* C,
                                     int32_t* status, hipStream_t stream) {
-    if (cls == 0)
-        return loop_multi_launch<1, TGMS_TWO_WAVE_MAX_M>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
-    return loop_multi_launch<TGMS_TWO_WAVE_MAX_M + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
+    if (ED) {
+        if (cls == 0) return loop_multi_launch<1, E>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+        return loop_multi_launch<E + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    }
+    if (cls == 0) return loop_multi_launch<1, A>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    return loop_multi_launch<A + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
 }
 
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
                                const double* T, const double* ED, double kT, double eta, double* Tout, double* cost,
                                double* C, int32_t* status, hipStream_t stream) {
-    if (cls == 0)
-        return multi_launch<1, TGMS_TWO_WAVE_MAX_M>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
-    return multi_launch<TGMS_TWO_WAVE_MAX_M + 1, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
+    if (ED) {
+        if (cls == 0) return multi_launch<1, E>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+        return multi_launch<E + 1, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    }
+    if (cls == 0) return multi_launch<1, A>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
+    return multi_launch<A + 1, 16>(tab, refine, so, W, T, ED, kT, eta, Tout, cost, C, status, stream);
 }
 
 #define TGMS_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
