@@ -120,6 +120,44 @@ def test_band_config3_device_matches_reduced(band):
     assert float(err.max()) <= TOL
 
 
+@pytest.mark.parametrize("B,M,seed", [(131072, 16, 7000), (131072, 16, 1), (40000, 16, 7000),
+                                      (131072, 10, 7000), (40000, 10, 7000), (40000, 3, 910)])
+def test_band_slab_reuse_at_round3_failing_shapes(band, oracle, B, M, seed):
+    """The shapes at which round 3's two-wave build returned wrong coefficients with status
+    OK (scripts/band_diag.py): every wavefront of the persistent grid solves
+    several 16-trajectory groups through its one U slab.  The shipped build, twice (the
+    failures varied run to run): every trajectory against the reduced solve, slices at the
+    start, the middle and the end against the oracle's dense GEPP (KKT_BAND)."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(B, M, seed=seed)
+    dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+    dR = torch.empty((B, M, 3, 8), dtype=torch.float64, device="cuda")
+    band.set_method(METHOD_REDUCED)
+    band.solve_uniform_device(B, M, dW, dT, dR, None)
+    band.set_method(METHOD_BAND_KKT)
+    dC = torch.empty_like(dR)
+    dS = torch.empty((B,), dtype=torch.int32, device="cuda")
+    for rep in range(2):
+        dC.fill_(np.nan)
+        dS.fill_(-1)
+        band.solve_uniform_device(B, M, dW, dT, dC, dS)
+        torch.cuda.synchronize()
+        assert int((dS != 0).sum()) == 0, rep
+        err = (dC - dR).abs().amax(dim=(1, 3)) / dR.abs().amax(dim=(1, 3))
+        nbad = int((~(err <= TOL)).sum())
+        assert nbad == 0, (rep, nbad, float(err.max()))
+    Wf, Tf = W.reshape(B, M + 1, 3), T.reshape(B, M)
+    C = dC.cpu().numpy()
+    for lo in (0, B // 2 - 128, B - 256):
+        sl = slice(lo, lo + 256)
+        so_s = np.arange(257, dtype=np.int32) * M
+        R, rst = oracle.solve_batch(so_s, Wf[sl].reshape(-1, 3), Tf[sl].reshape(-1), None, oracle.KKT_BAND)
+        assert (rst == 0).all()
+        assert batch_rel_err(so_s, C[sl].reshape(-1, 3, 8), R) <= TOL
+
+
 def test_band_ragged_end_derivs_and_invalid(band, oracle):
     """A ragged batch (every M in 1..16, groups solved one after another through the
     shared U slabs) with end derivatives and invalid trajectories in several groups:
