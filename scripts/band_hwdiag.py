@@ -37,7 +37,7 @@ for rep in range(REPS):
         n = 1 << w
         out[f] = {"all": np.bincount(v, minlength=n).tolist(), "bad": np.bincount(v[bad], minlength=n).tolist()}
     # distinct (xcc, se, sh, cu) places and how many workgroup slots each used
-    place = (hw >> 8) & 0xFFF | (((hw >> 20) & 0xF) << 12)
+    place = (hw >> 8) & 0xFF | (((hw >> 20) & 0xF) << 8)  # CU, SH, SE, XCC (not the workgroup slot)
     tg = (hw >> 16) & 0xF
     pt = np.unique(place * 16 + tg)
     cnt = np.bincount(pt // 16)

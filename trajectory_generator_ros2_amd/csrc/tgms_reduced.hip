@@ -519,6 +519,13 @@ template <class T>
 struct is_grad : std::false_type {};
 template <int NE>
 struct is_grad<GradAcc<NE>> : std::true_type {};
+// The refinement loop's last pass: the coefficients at the final times AND the cost there
+// (the sum of this lane's J only) from one solve, instead of a cost pass and a separate
+// emission pass.
+struct CostOut {
+    OutCtx o;
+    mutable double J;
+};
 
 
 // The same J and dJ/dT from the segment's scaled monomial data P4..P7 (c_k = r^(k-3) P_k)
@@ -544,6 +551,14 @@ __device__ __forceinline__ void seg_cost_p(double D, double V0, double A0, doubl
     Q = P4 * H4 + P5 * H5 + P6 * H6 + P7 * H7;
     const double G = Q4 * H4 + Q5 * H5 + Q6 * H6 + Q7 * H7;
     Qd = -(Q + 2.0 * G);
+}
+// Q alone (the cost at the final times needs no derivative): 20 FP64 operations.
+__device__ __forceinline__ double seg_cost_q(double P4, double P5, double P6, double P7) {
+    const double H4 = 576.0 * P4 + 1440.0 * P5 + 2880.0 * P6 + 5040.0 * P7;
+    const double H5 = 1440.0 * P4 + 4800.0 * P5 + 10800.0 * P6 + 20160.0 * P7;
+    const double H6 = 2880.0 * P4 + 10800.0 * P5 + 25920.0 * P6 + 50400.0 * P7;
+    const double H7 = 5040.0 * P4 + 20160.0 * P5 + 50400.0 * P6 + 100800.0 * P7;
+    return P4 * H4 + P5 * H5 + P6 * H6 + P7 * H7;
 }
 
 // Coefficients of axis a of virtual segment e (virtual knots e, e+1 with derivatives
@@ -606,7 +621,12 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
         for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
-        if constexpr (__is_same(Out, OutBuf))
+        if constexpr (__is_same(Out, CostOut)) {
+            const bool mine = has_r || !right;  // as for GradAcc
+            o.J += mine ? r * seg_cost_q(P4, P5, P6, P7) : 0.0;
+            asm volatile("" : "+v"(o.J));
+            stage_axis(o.o, c, a, e, M - 1 - e, has_r);
+        } else if constexpr (__is_same(Out, OutBuf))
             stage_axis(o, c, a, out_step(o, e), has_r);
         else
             stage_axis(o, c, a, e, M - 1 - e, has_r);
@@ -1405,6 +1425,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
     int32_t st_last = TGMS_OK;
     for (int32_t it = 0; it <= iters; ++it) {  // it == iters: the cost at the final times
         const LaneView L = make_view<M>(sm.in, slot, right);
+        if (C && it == iters) break;  // the last pass follows the loop
         GradAcc<NE> G;
 #pragma unroll
         for (int e = 0; e < NE; ++e) G.J[e] = G.dJ[e] = 0.0;
@@ -1436,20 +1457,35 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         }
         __syncthreads();
     }
+    if (C) {
+        const LaneView L = make_view<M>(sm.in, slot, right);
+        // the last pass: the coefficients at the final times and the cost there from
+        // one solve (a separate cost pass and emission pass before: 12 -> 11 solves
+        // per trajectory at 10 steps)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            if (live && valid && e < nmine) T[s0 + (right ? M - 1 - e : e)] = Tl[e];
+        }
+        // kT sum T first: the times are dead during the solve
+        double Ft = 0.0;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            if (live && e < nmine) Ft += kT * Tl[e];
+        }
+        const CostOut O{make_out(sm.O, sm.in.base, C, nb, lane), 0.0};
+        const int32_t st = pair_solve<M, HAS_ED, CostOut>(L, right, valid, ed, O);
+        const double Fl = live ? O.J + Ft : 0.0;
+        const double F = Fl + pair_swap(Fl);
+        if (live && !right && cost) cost[b] = F;
+        if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + sm.in.base[slot], M * 24, right, 2);
+        if (live && !right && status) status[b] = st;
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         if (live && valid && e < nmine) T[s0 + (right ? M - 1 - e : e)] = Tl[e];
     }
-    if (C) {
-        __syncthreads();
-        const LaneView L = make_view<M>(sm.in, slot, right);
-        const OutCtx O = make_out(sm.O, sm.in.base, C, nb, lane);
-        const int32_t st = pair_solve<M, HAS_ED, OutCtx>(L, right, valid, ed, O);
-        if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + sm.in.base[slot], M * 24, right, 2);
-        if (live && !right && status) status[b] = st;
-    } else if (live && !right && status) {
-        status[b] = st_last;
-    }
+    if (live && !right && status) status[b] = st_last;
 }
 
 template <int M, bool HAS_ED>
