@@ -18,7 +18,7 @@
 // per-trajectory slab in slot order; back substitution (back_step) by 8-lane groups
 // reads it back 16 + 8 B per lane and row.  Round 2's row-lane mapping (a 16-lane DPP row
 // per trajectory, LDS pivot-row broadcast) took 1.56-1.61 ms per 65,536 at M = 10; this
-// one 1.33 ms.
+// one 1.33 ms at one wavefront per SIMD, 1.22 ms at two.
 #include <algorithm>
 
 #include "tgms_device.h"
@@ -146,14 +146,21 @@ constexpr int QL = 4;                   // forward elimination: lanes per trajec
 constexpr int QTW = W64 / QL;           // trajectories per wavefront
 constexpr int NJ = 6;                   // registers per window row and lane (slots 4 j + q)
 constexpr int QW = 4;                   // wavefronts per workgroup (share the pattern table)
-// One wavefront per SIMD: the window (120 VGPRs), the masks, multipliers, pivot and
-// entering rows need ~290 registers; squeezed into 256 for two wavefronts per SIMD the
-// kernel spills, and the spilling build returned wrong results for the second workgroup
-// on a CU in measured runs, so the kernel runs at one wavefront per SIMD
-// with the AGPRs as register space and no scratch.
+// Two wavefronts per SIMD (two workgroups per CU, TGMS_BAND_WAVES_PER_CU = 8): the window
+// (120 VGPRs), masks, multipliers, pivot and entering rows need ~290 registers, so within
+// 256 the compiler spills ~37 VGPRs (144 B of scratch per lane, a few per step);
+// the second wavefront hides the one-wave build's exposed step latency: 1.22 vs 1.28-1.32 ms
+// per 65,536 at M = 10.  Round 3 shipped one wavefront per SIMD after
+// an intermediate two-wave build returned wrong results; round 4 could not reproduce that
+// with any committed source (HW_ID-tagged runs at two workgroups per CU,
+// every shape that failed, three runs each, all exact), and tests/test_gpu_band.py checks
+// those shapes on every GPU run.  TGMS_BAND_WAVES_PER_EU=1 with TGMS_BAND_WAVES_PER_CU=4
+// builds the round-3 configuration (AGPRs as register space, no scratch).
 #ifndef TGMS_BAND_WAVES_PER_EU
-#define TGMS_BAND_WAVES_PER_EU 1
+#define TGMS_BAND_WAVES_PER_EU 2
 #endif
+static_assert(TGMS_BAND_WAVES_PER_EU * 4 <= BAND_WAVES_PER_CU,  // 4 SIMDs per CU
+              "the persistent grid and the slab scratch must cover every resident wavefront");
 
 // Per-trajectory LDS block: Vc (the entering row's segment) | T | waypoints | end derivs.
 // Vc = [1, T^0..T^7 (0..8), 2 T^e / e for e = 1..7 (9..15), 0, 0, 0 (16..18)]
@@ -422,73 +429,6 @@ __device__ __forceinline__ void back_step(int k, int l0, int g, __amdgpu_buffer_
     ld_slots(rs, slot_off(g, k - WC, N), l, ra[S], rb[S]);
 }
 
-// Back substitution by the forward quad (round 4): the four lanes of a trajectory read back
-// exactly the slots they stored (registers j = 0..5, slot 4 j + q: two 16-B and two 8-B
-// loads per row, the second 8-B one out of range for q >= 2), so all sixteen trajectories
-// of the wave go in ONE pass of N dependent steps instead of two passes of eight: per step
-// six FMAs per axis and a two-stage DPP quad reduction.  The solution window is the same
-// slot window (x_c in slot c mod 19; slots 19..21 the constants -1 of their axis).  Rows
-// come through a 19-deep ring of loads issued a lap ahead.
-#ifndef TGMS_BAND_BACK4
-#define TGMS_BAND_BACK4 0  // 1 after GPU validation
-#endif
-struct Ring4 {
-    double2 a, b;  // registers (0, 2) and (1, 3)
-    double c, d;   // registers 4 and 5
-};
-
-__device__ __forceinline__ void ld_row4(__amdgpu_buffer_rsrc_t rs, int kk, int N, uint32_t vrow, uint32_t vrow1,
-                                        uint32_t vrow5, Ring4& r) {
-    // row kk of this lane's trajectory (rows before 0: out of range, read as 0)
-    const bool in = kk >= 0;
-    const uint32_t so = in ? (uint32_t)(kk * SW * 8) : 0u;
-    const uint32_t oob = 0x7FFFFF00u;
-    r.a = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, in ? vrow + so : oob, 0, BCPOL_SC1));
-    r.b = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, in ? vrow + 64u + so : oob, 0, BCPOL_SC1));
-    r.c = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, in ? vrow1 + so : oob, 0, BCPOL_SC1));
-    r.d = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (in && vrow5 != oob) ? vrow5 + so : oob,
-                                                                            0, BCPOL_SC1));
-}
-
-template <int M, int S>
-__device__ __forceinline__ void back_step4(int k, int q0, __amdgpu_buffer_rsrc_t rs, uint32_t vrow, uint32_t vrow1,
-                                           uint32_t vrow5, Ring4 (&ring)[WC], double (&x)[NJ][3], double* out,
-                                           bool live, bool emit, double& fin) {
-    constexpr int N = 14 * M + 2;
-    constexpr int R = ((N - 1 - S) % WC + WC) % WC;  // slot of column k
-    constexpr int RI = R / QL, RL = R % QL;
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    const int q = opaque(q0);
-    const Ring4 u = ring[S];
-    double sm[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double s0 = fma(u.b.x, x[1][a], u.a.x * x[0][a]);
-        const double s1 = fma(u.b.y, x[3][a], u.a.y * x[2][a]);
-        sm[a] = fma(u.d, x[5][a], fma(u.c, x[4][a], s0)) + s1;
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        sm[a] += dpp_f64<0xB1>(sm[a]);  // quad_perm [1,0,3,2]
-        sm[a] += dpp_f64<0x4E>(sm[a]);  // quad_perm [2,3,0,1]
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) x[RI][a] = (q == RL) ? -sm[a] : x[RI][a];
-    if (q == 0 && k >= 0) {
-        fin += (sm[0] + sm[1] + sm[2]) * 0.0;
-        const Pos pk = decode<M>(k);
-        if (pk.kind == 1 && live) {
-            double* o = out + pk.seg * 24 + pk.idx;
-            o[0] = emit ? -sm[0] : 0.0;
-            o[8] = emit ? -sm[1] : 0.0;
-            o[16] = emit ? -sm[2] : 0.0;
-        }
-    }
-    // refill the ring slot for step k-19 (same slot)
-    ld_row4(rs, k - WC, N, vrow, vrow1, vrow5, ring[S]);
-}
-
 template <int M, bool HAS_ED>
 __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_BAND_WAVES_PER_EU))) void k_band_kkt(
     int32_t n_traj, const int32_t* __restrict__ ids, const int32_t* __restrict__ seg_offsets,
@@ -585,63 +525,6 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         }
         const unsigned long long singm = __ballot(sing);
 
-#if TGMS_BAND_BACK4
-        // ---- back substitution by the quad, all sixteen trajectories in one pass: every
-        // lane reads back only the slab slots it stored itself (after its own stores have
-        // completed: vmcnt(0)); L1-bypassing loads as the slab is reused by the next group
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        {
-            constexpr int kN = N - 1;
-            const int q = opaque(lane % QL);
-            const int bq = QTW * grp + g;
-            const bool liveq = bq < n_traj;
-            const int32_t bb = ids ? ids[liveq ? bq : QTW * grp] : (liveq ? bq : QTW * grp);
-            const int64_t sq = seg_offsets ? (int64_t)seg_offsets[bb] : (int64_t)bb * M;
-            const bool valid = ((badm >> (QL * g)) & 0xfull) == 0;
-            const bool singular = ((singm >> (QL * g)) & 0xfull) != 0;
-            const bool emit = liveq && valid && !singular;
-            Ring4 ring[WC];
-#pragma unroll
-            for (int S = 0; S < WC; ++S) ld_row4(rs, kN - S, N, vrow, vrow1, vrow5, ring[S]);
-            // slots 19, 20, 21 (register 4 of lane 3, register 5 of lanes 0 and 1): -1 for their axis
-            double x[NJ][3];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                for (int a = 0; a < 3; ++a) x[j][a] = (4 * j + q == 19 + a) ? -1.0 : 0.0;
-            double* out = C + sq * 24;
-            double fin = 0.0;
-            for (int k0 = kN; k0 >= 0; k0 -= WC) {
-#define BSTEP(S) back_step4<M, S>(k0 - S, q, rs, vrow, vrow1, vrow5, ring, x, out, liveq, emit, fin);
-                BSTEP(0) BSTEP(1) BSTEP(2) BSTEP(3) BSTEP(4) BSTEP(5) BSTEP(6) BSTEP(7) BSTEP(8) BSTEP(9)
-                BSTEP(10) BSTEP(11) BSTEP(12) BSTEP(13) BSTEP(14) BSTEP(15) BSTEP(16) BSTEP(17) BSTEP(18)
-#undef BSTEP
-            }
-            const unsigned long long nf = __ballot(!(fin == 0.0));
-            const bool nonfinite = ((nf >> (QL * g)) & 0xfull) != 0;
-            if (liveq && q == 0 && status) {
-                int32_t st = TGMS_OK;
-                if (!valid) st = TGMS_ERR_INVALID_ARG;
-                else if (singular) st = TGMS_ERR_SINGULAR;
-                else if (nonfinite) st = TGMS_ERR_NONFINITE;
-#ifdef TGMS_BAND_HWID  // diagnosis build (scripts/band_hwdiag.py): where the trajectory ran
-                uint32_t hw, xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                st = (int32_t)((hw & 0x000FFFFFu) | ((xcc & 0xFu) << 20) | ((uint32_t)(st & 0xF) << 24));
-#endif
-                status[bb] = st;
-            }
-            // a non-finite solution is rewritten as exact zeros, like every other failure
-            // (its coefficients were stored during the sweep): rare path, after this
-            // wave's own stores to the range have completed
-            if (liveq && valid && !singular && nonfinite) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const int64_t mq = seg_offsets ? (int64_t)seg_offsets[bb + 1] - sq : M;
-                for (int64_t e = q; e < mq * 24; e += QL) out[e] = 0.0;
-            }
-        }
-#else
         // ---- back substitution (round 3), 8-lane groups, eight trajectories per pass.  The U rows
         // this wave stored are read back by other lanes of the wave: wait for the stores to
         // reach L2 and read them with L1-bypassing loads (the slab is reused by the next
@@ -708,7 +591,6 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
                 for (int64_t e = lb; e < mq * 24; e += BL) out[e] = 0.0;
             }
         }
-#endif
 #ifdef TGMS_BAND_FENCE
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
 #endif

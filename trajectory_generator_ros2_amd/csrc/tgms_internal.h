@@ -41,10 +41,10 @@ hipError_t launch_dense_kkt(int M, int32_t n_traj, const int32_t* traj_ids /*nul
 // Band-KKT solve (the same KKT and partial-pivoting LU, segment-interleaved order, the
 // structurally-zero entries skipped): sixteen trajectories per wavefront, persistent grid
 // of `grid` wavefronts, each with private U slabs in `scratch` (band_scratch_bytes).
-// grid = CUs x BAND_WAVES_PER_CU (the scratch is sized for it: one wavefront per SIMD,
-// the register budget of the kernel); the launch uses the resident part of it.
+// grid = CUs x BAND_WAVES_PER_CU (the scratch is sized for it: two wavefronts per SIMD,
+// the kernel's register budget); the launch uses the resident part of it.
 #ifndef TGMS_BAND_WAVES_PER_CU
-#define TGMS_BAND_WAVES_PER_CU 4
+#define TGMS_BAND_WAVES_PER_CU 8
 #endif
 constexpr int BAND_WAVES_PER_CU = TGMS_BAND_WAVES_PER_CU;
 size_t band_scratch_bytes(int M, int32_t grid);
