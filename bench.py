@@ -284,7 +284,7 @@ def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_
                             "flops_source": f"{C5_PMC_FILE} (executed FP64 flops, rocprofv3 --pmc of "
                                             f"scripts/c5bench.py: the same call), / this run's event time",
                             "valu_issue_frac": pmc["valu_insts_per_call"] * 4 / (1024 * 2.4e9 * ms * 1e-3),
-                            "hbm": hbm, "kernels": "k_refine_loop_multi<1,11> + <12,16>, concurrent"}
+                            "hbm": hbm, "kernels": "k_refine_loop_multi<1,13> (two waves per SIMD) + <14,16> (one), concurrent"}
     else:
         line["roofline"] = {"bound": "fp64_valu", "achieved": None, "hbm": hbm}
     return line

@@ -15,7 +15,9 @@ for f in glob.glob(f"{src}/p*/**/*counter_collection.csv", recursive=True):
         k = r["Kernel_Name"]
         if "k_refine_loop_multi" not in k:
             continue
-        cls = "k_refine_loop_multi<12,16>" if "<12, 16" in k or "ILi12ELi16E" in k else "k_refine_loop_multi<1,11>"
+        import re
+        m = re.search(r"k_refine_loop_multi<(\d+), (\d+)", k)
+        cls = f"k_refine_loop_multi<{m.group(1)},{m.group(2)}>" if m else "k_refine_loop_multi"
         acc[cls][r["Counter_Name"]].append(float(r["Counter_Value"]))
 kern = {c: {n: sum(v) / len(v) for n, v in d.items()} for c, d in acc.items()}
 tot = collections.Counter()

@@ -7,14 +7,16 @@
 namespace tgms {
 
 // Largest M solved at two wavefronts per SIMD (the axis-sequential state of larger M
-// needs more than 256 registers); ragged batches launch one kernel per class.
+// needs more than 256 registers); ragged batches launch one kernel per class.  13: the
+// fused refinement loop keeps 4 VGPRs in scratch at M = 12..13 and still beats running
+// them at one wave (config 5: 0.489-0.494 against 0.494-0.506 ms with 11, round 4).
 #ifndef TGMS_TWO_WAVE_MAX_M
-#define TGMS_TWO_WAVE_MAX_M 11
+#define TGMS_TWO_WAVE_MAX_M 13
 #endif
-// ... and with end derivatives (their extra state spills the fused refinement loop at
-// M = 11 within 256 registers; M <= 10 fits with none)
+// ... and with end derivatives (their extra state spills the fused refinement loop by
+// 79 VGPRs at M = 12..13 within 256 registers; M <= 11 fits with none)
 #ifndef TGMS_TWO_WAVE_MAX_M_ED
-#define TGMS_TWO_WAVE_MAX_M_ED 10
+#define TGMS_TWO_WAVE_MAX_M_ED 11
 #endif
 constexpr int two_wave_max_m(bool has_ed) { return has_ed ? TGMS_TWO_WAVE_MAX_M_ED : TGMS_TWO_WAVE_MAX_M; }
 
