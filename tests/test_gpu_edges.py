@@ -161,3 +161,49 @@ def test_overflow_reports_nonfinite_and_writes_zeros(solver, method, M):
         assert (st[others] == OK).all(), st
         for b in others:
             assert np.isfinite(C[so_r[b]: so_r[b + 1]]).all()
+
+
+def test_ragged_nan_end_derivative_is_invalid(solver, oracle):
+    """A non-finite end derivative is a non-finite input (include/tgms.h): on the ragged
+    lane-pair paths (every M class) the trajectory is flagged TGMS_ERR_INVALID_ARG and comes
+    out as exact zeros, and the refinement loop leaves its times alone; the other
+    trajectories are unaffected (bit-equal to the batch with the NaNs replaced)."""
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    solver.set_method(METHOD_REDUCED)
+    rng = np.random.default_rng(5150)
+    so, W, T = S.ragged_batch(1200, 1, 16, seed=5150)
+    B = len(so) - 1
+    M = np.diff(so)
+    ED = rng.normal(size=(B, 18))
+    bad = [int(np.flatnonzero(M == m)[1]) for m in (1, 2, 7, 11, 12, 13, 14, 16)]
+    ED_ok = ED.copy()
+    for i, b in enumerate(bad):
+        ED[b, (5 * i) % 18] = np.nan if i % 2 else np.inf
+    C, st, worst = solver.solve(so, W, T, ED)
+    assert worst == ERR_INVALID_ARG
+    assert all(st[b] == ERR_INVALID_ARG for b in bad)
+    good = np.setdiff1d(np.arange(B), bad)
+    assert (st[good] == 0).all()
+    for b in bad:
+        assert (C[so[b]:so[b + 1]] == 0.0).all()
+    C2, _, _ = solver.solve(so, W, T, ED_ok)
+    for b in good:
+        assert np.array_equal(C[so[b]:so[b + 1]], C2[so[b]:so[b + 1]])
+    R, _ = oracle.solve_batch(so, W, T, ED_ok, oracle.REDUCED)
+    for b in good[:200]:
+        sl = slice(so[b], so[b + 1])
+        assert batch_rel_err([0, so[b + 1] - so[b]], C[sl], R[sl]) <= TOL
+    # the refinement loop: the invalid trajectories keep their times and come out as zeros
+    T1, C1, cost1, st1, w1 = solver.refine(so, W, T, ED, iters=10)
+    T2, C2, cost2, st2, _ = solver.refine(so, W, T, ED_ok, iters=10)
+    assert w1 == ERR_INVALID_ARG
+    assert all(st1[b] == ERR_INVALID_ARG for b in bad)
+    assert (st1[good] == 0).all()
+    for b in bad:
+        assert np.array_equal(T1[so[b]:so[b + 1]], np.asarray(T).reshape(-1)[so[b]:so[b + 1]])
+        assert (C1[so[b]:so[b + 1]] == 0.0).all()
+    for b in good:
+        assert np.array_equal(T1[so[b]:so[b + 1]], T2[so[b]:so[b + 1]])
+        assert np.array_equal(C1[so[b]:so[b + 1]], C2[so[b]:so[b + 1]])
+        assert cost1[b] == cost2[b]

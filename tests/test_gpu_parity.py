@@ -347,18 +347,19 @@ def test_device_slices_and_alignment(solver):
     assert e.value.status == ERR_INVALID_ARG and "aligned" in solver.last_error()
 
 
-@pytest.mark.parametrize("M", [2, 4, 10, 16])
+@pytest.mark.parametrize("M", [2, 4, 10, 12, 14, 16, 5, 13])
 def test_lane_kernel_end_derivs_invalid_and_tail(solver, oracle, M):
-    """The lane-per-trajectory kernel (uniform batches, even M): end derivatives, a
-    partial last wavefront (B = 3 x 64 + 5) whose waypoint array has an odd number of
-    doubles (the last one outside every 16-B LDS-DMA piece), and invalid trajectories
-    in several wavefronts — T <= 0, non-finite T, a NaN waypoint, a NaN end derivative.
-    Valid trajectories match the oracle; invalid ones are flagged and come out as
-    exact zeros."""
+    """Uniform batches with end derivatives on the lane-per-trajectory kernel (even M <= 12)
+    and the lane-pair kernel (odd M, M >= 14): a partial last wavefront (B = 3 x 64 + 5;
+    for even M the waypoint array has an odd number of doubles, the last one outside
+    every 16-B LDS-DMA piece), and invalid trajectories in several wavefronts — T <= 0,
+    non-finite T, a NaN waypoint, a NaN end derivative.  Valid trajectories match the
+    oracle; invalid ones are flagged TGMS_ERR_INVALID_ARG (a NaN end derivative is a
+    non-finite input, include/tgms.h) and come out as exact zeros."""
     from trajectory_generator_ros2_amd import ERR_INVALID_ARG
     B = 3 * 64 + 5
     so, W, T = _uniform(B, M, seed=900 + M)
-    assert (W.size % 2) == 1
+    assert (W.size % 2) == (M + 1) % 2
     rng = np.random.default_rng(900 + M)
     ED = rng.normal(size=(B, 18))
     T = T.copy(); W = W.copy()

@@ -522,10 +522,16 @@ struct is_grad<GradAcc<NE>> : std::true_type {};
 // The refinement loop's last pass: the coefficients at the final times AND the cost there
 // (the sum of this lane's J only) from one solve, instead of a cost pass and a separate
 // emission pass.
-struct CostOut {
-    OutCtx o;
+template <class O>
+struct CostOutT {
+    O o;
     mutable double J;
 };
+using CostOut = CostOutT<OutCtx>;
+template <class T>
+struct is_cost_out : std::false_type {};
+template <class O>
+struct is_cost_out<CostOutT<O>> : std::true_type {};
 
 
 // The same J and dJ/dT from the segment's scaled monomial data P4..P7 (c_k = r^(k-3) P_k)
@@ -587,6 +593,16 @@ __device__ __forceinline__ void row_coeffs(const LaneView& L, bool right, int e,
     c[7] = P7 * r4;
 }
 
+// Where one axis of segment e goes, per output kind.
+template <int M>
+__device__ __forceinline__ void emit_c(const OutBuf& o, const double (&c)[8], int a, int e, bool has_r) {
+    stage_axis(o, c, a, out_step(o, e), has_r);
+}
+template <int M>
+__device__ __forceinline__ void emit_c(const OutCtx& o, const double (&c)[8], int a, int e, bool has_r) {
+    stage_axis(o, c, a, e, M - 1 - e, has_r);
+}
+
 template <int M, class Out>
 __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
                                           const double (&xs)[3], const double (&xe)[3], bool has_r,
@@ -621,15 +637,14 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
         for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
-        if constexpr (__is_same(Out, CostOut)) {
+        if constexpr (is_cost_out<Out>::value) {
             const bool mine = has_r || !right;  // as for GradAcc
             o.J += mine ? r * seg_cost_q(P4, P5, P6, P7) : 0.0;
             asm volatile("" : "+v"(o.J));
-            stage_axis(o.o, c, a, e, M - 1 - e, has_r);
-        } else if constexpr (__is_same(Out, OutBuf))
-            stage_axis(o, c, a, out_step(o, e), has_r);
-        else
-            stage_axis(o, c, a, e, M - 1 - e, has_r);
+            emit_c<M>(o.o, c, a, e, has_r);
+        } else {
+            emit_c<M>(o, c, a, e, has_r);
+        }
     }
 }
 
@@ -797,6 +812,14 @@ __device__ __forceinline__ void zero_traj(double* c, int n, int first, int step)
 // arithmetic into one block after the last scheduling fence (which only orders the
 // machine scheduler).
 __device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin_ldl3(Ldl3& f) {
+    pin(f.i0);
+    pin(f.i1);
+    pin(f.i2);
+    pin(f.l10);
+    pin(f.l20);
+    pin(f.l21);
+}
 __device__ __forceinline__ void pin33(double (&m)[3][3]) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -1050,6 +1073,17 @@ __device__ __forceinline__ void stage_row_t(In<M>& sm, int t, int q, double v) {
     if (!finite_pos(v)) atomicOr(&sm.bad[t], 1);
 }
 
+// A non-finite end derivative makes the trajectory invalid like a non-finite waypoint
+// (TGMS_ERR_INVALID_ARG, exact zeros; the lane and band kernels check the same): the two
+// lanes of the pair check 9 values each.
+template <int M>
+__device__ __forceinline__ void stage_check_ed(In<M>& sm, int t, bool right, const double* __restrict__ ed) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) bad = bad || !finite(ed[2 * q + right]);
+    if (bad) atomicOr(&sm.bad[t], 1);
+}
+
 // Invalid trajectories are replaced by an all-zero, unit-time one (whose solution
 // is exactly zero), so the solver needs no per-coefficient masking.  Rare path.
 template <int M>
@@ -1075,6 +1109,7 @@ struct RawLoader {
     double wl, tl;
     bool oddW, oddT, anyT;
     int nw, nt;
+    const double* ed = nullptr;  // end derivatives [B][18] (nullptr: rest-to-rest)
 
     __device__ __forceinline__ void issue(const double* __restrict__ W, const double* __restrict__ T, int32_t B,
                                           int64_t b0, int nb, int lane) {
@@ -1114,6 +1149,8 @@ struct RawLoader {
                 const double* t = T + (b0 + lane) * M;
                 for (int q = 0; q < NW; ++q) f |= !finite(w[q]);
                 for (int q = 0; q < M; ++q) f |= !finite_pos(t[q]);
+                if (ed)
+                    for (int q = 0; q < 18; ++q) f |= !finite(ed[(b0 + lane) * 18 + q]);
             }
             sm.bad[lane] = f;
             if (f)
@@ -1135,6 +1172,11 @@ struct RawLoader {
         if (oddT) {
             if (lane == 0) sm.R[nt - 1] = fast_rcp(tl);
             bad = bad || !finite_pos(tl);
+        }
+        if (ed && (lane >> 1) < nb) {  // a trajectory's end derivatives: 9 values per lane of its pair
+            const double* e = ed + (b0 + (lane >> 1)) * 18 + (lane & 1);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) bad = bad || !finite(e[2 * q]);
         }
         anyT = __builtin_amdgcn_ballot_w64(bad) != 0;
         if (anyT) flags(sm, W, T, b0, nb, lane);
@@ -1170,8 +1212,9 @@ struct RawLoader {
 
 template <int M>
 __device__ __forceinline__ bool stage_raw(RawIn<M>& sm, const double* __restrict__ W, const double* __restrict__ T,
-                                          int32_t B, int64_t b0, int nb, int lane) {
+                                          const double* __restrict__ ED, int32_t B, int64_t b0, int nb, int lane) {
     RawLoader<M> ld;
+    ld.ed = ED;
     ld.issue(W, T, B, b0, nb, lane);
     ld.stage_T(sm, W, T, b0, nb, lane);
     return ld.stage_W(sm, W, T, b0, nb, lane);
@@ -1190,6 +1233,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
     const int64_t b0 = (int64_t)blockIdx.x * TPW;
     const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
     RawLoader<M> ld;
+    ld.ed = HAS_ED ? ED : nullptr;
     ld.issue(W, T, B, b0, nb, lane);
     ld.stage_T(sm.in, W, T, b0, nb, lane);
     STAMP(1);
@@ -1260,7 +1304,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_uniform(int32_t B,
     const int lane = threadIdx.x;
     const int64_t b0 = (int64_t)blockIdx.x * TPW;
     const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
-    const bool any_bad = stage_raw<M>(sm, W, T, B, b0, nb, lane);
+    const bool any_bad = stage_raw<M>(sm, W, T, HAS_ED ? ED : nullptr, B, b0, nb, lane);
     const int slot = lane >> 1;
     const bool right = lane & 1;
     const bool live = slot < nb;
@@ -1303,6 +1347,7 @@ __device__ __forceinline__ void refine_ragged_block(Stage<M>& sm, int64_t blk, i
         const double* gW = W + (s0 + b) * 3;
         for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
         for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
+        if (HAS_ED) stage_check_ed(sm.in, slot, right, ED + (int64_t)b * 18);
     }
     __syncthreads();
     sanitize(sm.in, lane);
@@ -1360,6 +1405,7 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
         // the two lanes of a pair split the trajectory's rows
         for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
         for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
+        if (HAS_ED) stage_check_ed(sm.in, slot, right, ED + (int64_t)b * 18);
     }
     __syncthreads();
     sanitize(sm.in, lane);
@@ -1409,6 +1455,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         const double* gW = W + (s0 + b) * 3;
         for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
         for (int q = right; q < M; q += 2) stage_row_t(sm.in, slot, q, T[s0 + q]);
+        if (HAS_ED) stage_check_ed(sm.in, slot, right, ED + (int64_t)b * 18);
     }
     // this lane updates the times of its half of the segments; between steps they live
     // in its registers (and as 1/T in the stage); an invalid trajectory keeps its times
@@ -1634,18 +1681,8 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(Group
 // Same block LDL^T as the oracle's reduced formulation (oracle/minsnap_oracle.c),
 // one-sided instead of twisted.
 
-// Anchor a value at this point of the instruction stream: it must be computed before
-// the (volatile, ordered) statement, so IR-level sinking cannot pile every knot's
-// arithmetic into one block after the last scheduling fence (which only orders the
-// machine scheduler): without the anchors the kernel needs > 700 registers.
-__device__ __forceinline__ void pin_ldl3(Ldl3& f) {
-    pin(f.i0);
-    pin(f.i1);
-    pin(f.i2);
-    pin(f.l10);
-    pin(f.l20);
-    pin(f.l21);
-}
+// The lane kernel anchors every knot's factors and elimination vectors (pin_ldl3,
+// pin33): without the anchors it needs > 700 registers.
 
 // LDS byte address of a __shared__ object.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -2121,9 +2158,12 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
 #define TGMS_LANE_UNIFORM 1
 #endif
 // Largest M on the lane kernel: its whole elimination state lives in registers, which
-// at M >= 12 spill to scratch (92-980 B per lane); those M take the lane-pair kernel.
+// at M >= 12 spill to scratch (92-980 B per lane).  At M = 12 it still matches the
+// lane-pair kernel (51.6 vs 52.4 us per 65,536, fresh batches); at 14 and 16 the pair is
+// faster (60 vs 77 us, 69 vs 109 us; profiles/r04_lane_vs_pair_M12_16.jsonl), so M >= 14
+// take the lane-pair kernel.
 #ifndef TGMS_LANE_MAX_M
-#define TGMS_LANE_MAX_M 16
+#define TGMS_LANE_MAX_M 12
 #endif
 template <int M>
 constexpr bool use_lane_kernel() {
