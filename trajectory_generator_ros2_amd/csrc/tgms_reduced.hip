@@ -512,8 +512,8 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
 // KH are antisymmetric between the ends, so only D = (w1 - w0) r^3 appears.
 template <int NE>
 struct GradAcc {
-    mutable double J[NE];   // per emission step of this lane: cost of its segment
-    mutable double dJ[NE];  // and its derivative in the segment's duration
+    mutable double J;       // this lane's snap cost (its segments; only the sum is used)
+    mutable double dJ[NE];  // per emission step of this lane: d cost / d duration of its segment
 };
 template <class T>
 struct is_grad : std::false_type {};
@@ -627,12 +627,12 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
         double Q, Qd;
         seg_cost_p(D, V0, A0, V1, A1, P4, P5, P6, P7, Q, Qd);
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
-        o.J[e] += mine ? r * Q : 0.0;
+        o.J += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
         // anchored here: nothing stores these sums until the step's update, so without
         // the anchor the compiler sinks every segment's cost arithmetic (and keeps all
         // knot data live for it) to the end of the solve
-        asm volatile("" : "+v"(o.J[e]), "+v"(o.dJ[e]));
+        asm volatile("" : "+v"(o.J), "+v"(o.dJ[e]));
     } else {
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
@@ -1271,13 +1271,13 @@ __device__ __forceinline__ void refine_update(const GradAcc<Chain<M>::NE>& G, bo
     constexpr int NE = CH::NE;
     const int nmine = right ? CH::nR : NE;
     double Tl[NE];
-    double Fl = 0.0;
+    double Fl = live ? G.J : 0.0;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         const int phys = right ? M - 1 - e : e;
         const bool mine = live && e < nmine;
         Tl[e] = mine ? Tin[phys] : 0.0;
-        Fl += mine ? G.J[e] + kT * Tl[e] : 0.0;
+        Fl += mine ? kT * Tl[e] : 0.0;
     }
     const double F = Fl + pair_swap(Fl);
     const bool ok = (st == TGMS_OK) && F > 0.0;
@@ -1312,8 +1312,9 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_refine_uniform(int32_t B,
     const bool valid = !any_bad || sm.bad[slot] == 0;
     const LaneView L = make_view_raw<M>(sm, slot, right);
     GradAcc<Chain<M>::NE> G;
+    G.J = 0.0;
 #pragma unroll
-    for (int e = 0; e < Chain<M>::NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+    for (int e = 0; e < Chain<M>::NE; ++e) G.dJ[e] = 0.0;
     const int32_t st =
         pair_solve<M, HAS_ED, GradAcc<Chain<M>::NE>>(L, right, valid, (HAS_ED && live) ? ED + b * 18 : ED, G);
     refine_update<M>(G, right, st, live, kT, eta, T + (live ? b : 0) * M, Tout + (live ? b : 0) * M,
@@ -1355,8 +1356,9 @@ __device__ __forceinline__ void refine_ragged_block(Stage<M>& sm, int64_t blk, i
     const bool valid = sm.in.bad[slot] == 0;
     const LaneView L = make_view<M>(sm.in, slot, right);
     GradAcc<Chain<M>::NE> G;
+    G.J = 0.0;
 #pragma unroll
-    for (int e = 0; e < Chain<M>::NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+    for (int e = 0; e < Chain<M>::NE; ++e) G.dJ[e] = 0.0;
     const int32_t st = pair_solve<M, HAS_ED, GradAcc<Chain<M>::NE>>(
         L, right, valid, (HAS_ED && live) ? ED + (int64_t)b * 18 : ED, G);
     refine_update<M>(G, right, st, live, kT, eta, T + s0, Tout + s0, cost ? cost + b : nullptr);
@@ -1474,14 +1476,15 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
         const LaneView L = make_view<M>(sm.in, slot, right);
         if (C && it == iters) break;  // the last pass follows the loop
         GradAcc<NE> G;
+        G.J = 0.0;
 #pragma unroll
-        for (int e = 0; e < NE; ++e) G.J[e] = G.dJ[e] = 0.0;
+        for (int e = 0; e < NE; ++e) G.dJ[e] = 0.0;
         const int32_t st = pair_solve<M, HAS_ED, GradAcc<NE>>(L, right, valid, ed, G);
         st_last = st;
-        double Fl = 0.0;
+        double Fl = live ? G.J : 0.0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
-            if (live && e < nmine) Fl += G.J[e] + kT * Tl[e];
+            if (live && e < nmine) Fl += kT * Tl[e];
         }
         const double F = Fl + pair_swap(Fl);
         if (it == iters) {
@@ -2243,7 +2246,8 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
     if (tab.ngroups <= 0) return hipSuccess;
     const unsigned grid = (unsigned)tab.blk_end[tab.ngroups - 1];
     if (grid == 0) return hipSuccess;
-    if (refine) {
+    if constexpr (MLO > MHI) return hipSuccess;  // an empty class
+    else if (refine) {
         if (ED)
             TGMS_LAUNCH((k_refine_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
                                kT, eta, Tout, cost, status);
@@ -2263,18 +2267,17 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
 
 }  // namespace
 
-template <int MLO, int MHI>
+// (instantiated only for the classes a call can launch: end derivatives use the ED
+// boundary, so e.g. <1, TWO_WAVE_MAX_M, true> never exists)
+template <int MLO, int MHI, bool HAS_ED>
 hipError_t loop_multi_launch(const GroupTable& tab, const int32_t* so, const double* W, double* T, const double* ED,
                              double kT, double eta, int32_t iters, double* cost, double* C, int32_t* status,
                              hipStream_t stream) {
     const unsigned grid = tab.ngroups ? (unsigned)tab.blk_end[tab.ngroups - 1] : 0u;
     if (grid == 0) return hipSuccess;
-    if (ED)
-        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, true>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
-                           ED, kT, eta, iters, cost, C, status);
-    else
-        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, false>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T,
-                           ED, kT, eta, iters, cost, C, status);
+    if constexpr (MLO <= MHI)  // (MLO > MHI: an empty class, every M at two waves)
+        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, HAS_ED>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
+                    kT, eta, iters, cost, C, status);
     return hipSuccess;
 }
 
@@ -2283,11 +2286,11 @@ hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_
                                     int32_t* status, hipStream_t stream) {
     constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
     if (ED) {
-        if (cls == 0) return loop_multi_launch<1, E>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
-        return loop_multi_launch<E + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+        if (cls == 0) return loop_multi_launch<1, E, true>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+        return loop_multi_launch<E + 1, 16, true>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
     }
-    if (cls == 0) return loop_multi_launch<1, A>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
-    return loop_multi_launch<A + 1, 16>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    if (cls == 0) return loop_multi_launch<1, A, false>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    return loop_multi_launch<A + 1, 16, false>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
 }
 
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
