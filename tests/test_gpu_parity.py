@@ -161,6 +161,40 @@ def test_invalid_inputs(solver):
     solver.set_method(0)
 
 
+def test_ragged_structural_errors_name_the_first_trajectory(solver):
+    """Ragged offsets are validated on the host in chunks (csrc/tgms_capi.hip check_offsets);
+    an error must still name the FIRST offending trajectory, with the status a sequential
+    scan gives: M outside 1..16 -> TGMS_ERR_INVALID_ARG, M above the method's limit ->
+    TGMS_ERR_UNSUPPORTED, whichever comes first."""
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_UNSUPPORTED, METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.ragged_batch(4001, 2, 9, seed=31)
+    M = np.diff(so).astype(np.int64)
+    for bad_b, bad_m, status in ((2999, 0, ERR_INVALID_ARG), (1500, 17, ERR_INVALID_ARG), (7, -3, ERR_INVALID_ARG)):
+        M2 = M.copy()
+        M2[bad_b] = bad_m
+        M2[3500] = 0  # a later offender: not the one reported
+        so2 = np.concatenate([[0], np.cumsum(M2)]).astype(np.int32)
+        _, _, w = solver.solve(so2, np.zeros((int(so2[-1]) + len(M2), 3)), np.ones(max(int(so2[-1]), 1)))
+        assert w == status
+        assert f"trajectory {bad_b} has {bad_m} segments" in solver.last_error(), solver.last_error()
+    # the dense KKT stops at M = 10: the first trajectory above it is named
+    M2 = M.copy()
+    M2[1234] = 12
+    M2[2345] = 17  # invalid, but after the unsupported one
+    so2 = np.concatenate([[0], np.cumsum(M2)]).astype(np.int32)
+    solver.set_method(METHOD_DENSE_KKT)
+    try:
+        _, _, w = solver.solve(so2, np.zeros((int(so2[-1]) + len(M2), 3)), np.ones(int(so2[-1])))
+    finally:
+        solver.set_method(METHOD_REDUCED)
+    assert w == ERR_UNSUPPORTED
+    assert "trajectory 1234 has 12 segments" in solver.last_error(), solver.last_error()
+    # and a valid ragged batch of the same size still solves (the chunked grouping is exact)
+    C, st, w = solver.solve(so, W, T)
+    assert w == 0 and (st == 0).all()
+
+
 def test_config3_full_size_properties(solver, oracle):
     """BASELINE config 3 at full size (B = 65,536, M = 10) through the device API:
     parity with the oracle on every trajectory + size-independent properties."""

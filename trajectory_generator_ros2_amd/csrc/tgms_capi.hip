@@ -41,6 +41,8 @@ struct tgms_handle {
     size_t ws_cap = 0;
     int32_t* d_perm = nullptr;  // ragged plan: trajectory ids grouped by M
     size_t perm_cap = 0;
+    int32_t* d_perm_hist = nullptr;  // the device-side grouping's per-block counts (refinement loop)
+    size_t perm_hist_cap = 0;
     int32_t* h_perm = nullptr;  // pinned staging of the plan
     size_t h_perm_cap = 0;
     hipEvent_t perm_ev = nullptr;  // guards h_perm reuse until the upload completed
@@ -64,13 +66,13 @@ struct tgms_handle {
     // into a HIP graph and replayed while its arguments and plan are unchanged
     struct LoopKey {
         int32_t B = -1, iters = 0;
-        const void *d_so, *dW, *dT, *dT2, *dED, *dC, *d_cost, *dSt, *d_perm;
+        const void *d_so, *dW, *dT, *dT2, *dED, *dC, *d_cost, *dSt, *d_perm, *d_hist;
         double k_T, eta;
         std::vector<int32_t> counts, starts;
         int uniform_m;
         bool operator==(const LoopKey& o) const {
             return B == o.B && iters == o.iters && d_so == o.d_so && dW == o.dW && dT == o.dT && dT2 == o.dT2 &&
-                   dED == o.dED && dC == o.dC && d_cost == o.d_cost && dSt == o.dSt && d_perm == o.d_perm &&
+                   dED == o.dED && dC == o.dC && d_cost == o.d_cost && dSt == o.dSt && d_perm == o.d_perm && d_hist == o.d_hist &&
                    k_T == o.k_T && eta == o.eta && counts == o.counts && starts == o.starts &&
                    uniform_m == o.uniform_m;
         }
@@ -167,42 +169,110 @@ tgms_status ensure_loop_ws(tgms_handle* h, size_t bytes) {
     return TGMS_OK;
 }
 
+// The device-side grouping of the refinement loop: the permutation buffer (shared with the
+// host-planned paths) and the per-block counts.
+tgms_status ensure_perm_device(tgms_handle* h, int32_t B) {
+    if ((size_t)B > h->perm_cap) {
+        if (h->d_perm) {
+            TGMS_HIP(h, hipDeviceSynchronize());
+            TGMS_HIP(h, hipFree(h->d_perm));
+            h->d_perm = nullptr;
+        }
+        TGMS_HIP(h, hipMalloc(reinterpret_cast<void**>(&h->d_perm), sizeof(int32_t) * B));
+        h->perm_cap = B;
+    }
+    const size_t need = tgms::perm_hist_bytes(B);
+    if (need > h->perm_hist_cap) {
+        if (h->d_perm_hist) {
+            TGMS_HIP(h, hipDeviceSynchronize());
+            TGMS_HIP(h, hipFree(h->d_perm_hist));
+            h->d_perm_hist = nullptr;
+        }
+        TGMS_HIP(h, hipMalloc(reinterpret_cast<void**>(&h->d_perm_hist), need));
+        h->perm_hist_cap = need;
+    }
+    return TGMS_OK;
+}
+
 // Validates a CSR segment layout on the host; fills per-M counts.
+// Host planning of ragged batches (a config-5 batch of 1,048,576 trajectories has to be
+// validated and grouped by M on every call): the offsets are scanned in PLAN_CHUNKS
+// contiguous chunks interleaved in one loop, so the per-chunk histogram updates (and the
+// counting-sort cursors below) form independent dependency chains instead of one.
+constexpr int PLAN_CHUNKS = 4;
+constexpr int PLAN_BINS = TGMS_MAX_SEGMENTS + 2;  // M clamped into 0..MAX+1: 0 and MAX+1 are "out of range"
+struct ChunkHist {
+    int32_t B = -1;
+    const int32_t* so = nullptr;
+    int32_t h[PLAN_CHUNKS][PLAN_BINS];
+};
+thread_local ChunkHist t_hist;  // the last ragged check_offsets of this thread, reused by upload_plan
+
+void chunk_hist(int32_t B, const int32_t* so, ChunkHist& ch) {
+    std::memset(ch.h, 0, sizeof ch.h);
+    const int32_t L = B / PLAN_CHUNKS;
+    auto bin = [](int32_t M) { return M < 0 ? 0 : (M > TGMS_MAX_SEGMENTS ? TGMS_MAX_SEGMENTS + 1 : M); };
+    for (int32_t i = 0; i < L; ++i)
+        for (int c = 0; c < PLAN_CHUNKS; ++c) {
+            const int32_t b = c * L + i;
+            ch.h[c][bin(so[b + 1] - so[b])]++;
+        }
+    for (int32_t b = PLAN_CHUNKS * L; b < B; ++b) ch.h[PLAN_CHUNKS - 1][bin(so[b + 1] - so[b])]++;
+    ch.B = B;
+    ch.so = so;
+}
+
 tgms_status check_offsets(tgms_handle* h, int32_t B, const int32_t* so, int max_m,
                           std::vector<int32_t>* counts, int* uniform_m) {
     if (B < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "B < 0");
     if (!so) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets is NULL");
     if (so[0] != 0) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets[0] != 0");
     if (counts) counts->assign(max_m + 1, 0);
-    // uniform batches (the common large case): one vectorisable pass over the offsets
+    // uniform batches (the common large case): one vectorisable pass over the offsets,
+    // in blocks so a ragged batch leaves it after its first block
     if (B > 0) {
         const int32_t M0 = so[1] - so[0];
         int32_t diff = 0;
-        for (int32_t b = 0; b < B; ++b) diff |= (so[b + 1] - so[b]) ^ M0;
+        for (int32_t b0 = 0; b0 < B && diff == 0; b0 += 4096) {
+            const int32_t e = std::min(B, b0 + 4096);
+            for (int32_t b = b0; b < e; ++b) diff |= (so[b + 1] - so[b]) ^ M0;
+        }
         if (diff == 0 && M0 >= 1 && M0 <= TGMS_MAX_SEGMENTS && M0 <= max_m) {
             if (counts) (*counts)[M0] = B;
             if (uniform_m) *uniform_m = M0;
             return TGMS_OK;
         }
     }
-    int um = -1;
-    for (int32_t b = 0; b < B; ++b) {
-        const int32_t M = so[b + 1] - so[b];
-        if (M < 1 || M > TGMS_MAX_SEGMENTS) {
-            char buf[128];
-            snprintf(buf, sizeof buf, "trajectory %d has %d segments (allowed 1..%d)", b, M,
-                     TGMS_MAX_SEGMENTS);
-            return set_err(h, TGMS_ERR_INVALID_ARG, buf);
+    ChunkHist& ch = t_hist;
+    chunk_hist(B, so, ch);
+    int32_t tot[PLAN_BINS] = {};
+    for (int c = 0; c < PLAN_CHUNKS; ++c)
+        for (int m = 0; m < PLAN_BINS; ++m) tot[m] += ch.h[c][m];
+    bool bad = tot[0] || tot[TGMS_MAX_SEGMENTS + 1];
+    for (int m = max_m + 1; m <= TGMS_MAX_SEGMENTS; ++m) bad = bad || tot[m];
+    if (bad) {  // rare: report the first offending trajectory, as a sequential scan would
+        ch.B = -1;
+        for (int32_t b = 0; b < B; ++b) {
+            const int32_t M = so[b + 1] - so[b];
+            if (M < 1 || M > TGMS_MAX_SEGMENTS) {
+                char buf[128];
+                snprintf(buf, sizeof buf, "trajectory %d has %d segments (allowed 1..%d)", b, M,
+                         TGMS_MAX_SEGMENTS);
+                return set_err(h, TGMS_ERR_INVALID_ARG, buf);
+            }
+            if (M > max_m) {
+                char buf[128];
+                snprintf(buf, sizeof buf, "trajectory %d has %d segments; method supports <= %d", b, M, max_m);
+                return set_err(h, TGMS_ERR_UNSUPPORTED, buf);
+            }
         }
-        if (M > max_m) {
-            char buf[128];
-            snprintf(buf, sizeof buf, "trajectory %d has %d segments; method supports <= %d", b, M, max_m);
-            return set_err(h, TGMS_ERR_UNSUPPORTED, buf);
-        }
-        if (counts) (*counts)[M]++;
-        um = (b == 0) ? M : (um == M ? M : 0);
     }
-    if (uniform_m) *uniform_m = um;
+    int um = 0;
+    for (int m = 1; m <= max_m; ++m) {
+        if (counts) (*counts)[m] = tot[m];
+        if (B > 0 && tot[m] == B) um = m;
+    }
+    if (uniform_m) *uniform_m = (B > 0) ? um : -1;
     return TGMS_OK;
 }
 
@@ -229,8 +299,27 @@ tgms_status upload_plan(tgms_handle* h, int32_t B, const int32_t* so,
         h->perm_cap = B;
     }
     TGMS_HIP(h, hipEventSynchronize(h->perm_ev));  // previous upload must have drained
-    std::vector<int32_t> fill(starts->begin(), starts->end());
-    for (int32_t b = 0; b < B; ++b) h->h_perm[fill[so[b + 1] - so[b]]++] = b;
+    // stable counting sort: chunk c's trajectories of each M follow chunk c-1's, and the
+    // PLAN_CHUNKS cursors advance independently
+    ChunkHist& ch = t_hist;
+    if (!(ch.B == B && ch.so == so)) chunk_hist(B, so, ch);
+    int32_t cur[PLAN_CHUNKS][PLAN_BINS];
+    for (int m = 0; m < PLAN_BINS; ++m) {
+        int32_t base = (m >= 1 && (size_t)m < counts.size()) ? (*starts)[m] : 0;
+        for (int c = 0; c < PLAN_CHUNKS; ++c) {
+            cur[c][m] = base;
+            base += ch.h[c][m];
+        }
+    }
+    const int32_t L = B / PLAN_CHUNKS;
+    int32_t* const perm = h->h_perm;
+    for (int32_t i = 0; i < L; ++i)
+        for (int c = 0; c < PLAN_CHUNKS; ++c) {
+            const int32_t b = c * L + i;
+            perm[cur[c][so[b + 1] - so[b]]++] = b;
+        }
+    for (int32_t b = PLAN_CHUNKS * L; b < B; ++b) perm[cur[PLAN_CHUNKS - 1][so[b + 1] - so[b]]++] = b;
+    ch.B = -1;  // the offsets may change before the next call
     TGMS_HIP(h, hipMemcpyAsync(h->d_perm, h->h_perm, sizeof(int32_t) * B, hipMemcpyHostToDevice, stream));
     TGMS_HIP(h, hipEventRecord(h->perm_ev, stream));
     return TGMS_OK;
@@ -1064,6 +1153,7 @@ void tgms_destroy(tgms_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     (void)hipDeviceSynchronize();
     if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->d_perm_hist) (void)hipFree(h->d_perm_hist);
     if (h->d_band) (void)hipFree(h->d_band);
     if (h->d_band_graph) (void)hipFree(h->d_band_graph);
     for (double* p : h->band_retired) (void)hipFree(p);
@@ -1347,9 +1437,19 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (s == TGMS_OK) s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
     double* T[2] = {dT, h->d_loop_ws};
-    s = plan_upload(h, B, h_so, &plan, st);
-    if (s != TGMS_OK) return s;
+    // the M grouping is computed on the device, inside the loop's graph (no host counting
+    // sort, no permutation upload per call)
+    t_hist.B = -1;  // (no host counting sort on this path)
+    if (plan.uniform_m == 0) {
+        plan.starts.assign(plan.counts.size() + 1, 0);
+        for (size_t m = 1; m < plan.counts.size(); ++m) plan.starts[m + 1] = plan.starts[m] + plan.counts[m];
+        s = ensure_perm_device(h, B);
+        if (s != TGMS_OK) return s;
+        plan.d_perm = h->d_perm;
+    }
     auto body = [&](hipStream_t q) -> tgms_status {
+        if (plan.uniform_m == 0)
+            TGMS_HIP(h, tgms::launch_group_perm(B, d_so, plan.starts.data(), h->d_perm_hist, h->d_perm, q));
         int cur = 0;
         tgms_status r = refine_loop(h, plan, B, d_so, dW, T, dED, k_T, eta, iters, dC, d_cost, dSt, q, &cur);
         if (r != TGMS_OK) return r;
@@ -1362,7 +1462,7 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
         return s != TGMS_OK ? s : scratch_release(h, st);
     }
     // launch-bound (K x groups small kernels): capture once, replay while nothing changed
-    tgms_handle::LoopKey key{B, iters, d_so, dW, dT, T[1], dED, dC, d_cost, dSt, h->d_perm, k_T, eta,
+    tgms_handle::LoopKey key{B, iters, d_so, dW, dT, T[1], dED, dC, d_cost, dSt, h->d_perm, h->d_perm_hist, k_T, eta,
                              plan.counts, plan.starts, plan.uniform_m};
     if (!(h->loop_exec && h->loop_key == key)) {
         if (h->loop_exec) {

@@ -86,6 +86,13 @@ hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_
                                     double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
                                     double* C, int32_t* status, hipStream_t stream);
 
+// The M-grouping permutation of a ragged batch computed on the device (stable counting
+// sort of the ids by so[b+1] - so[b]; M validated on the host): starts[m] (m = 1..16) is
+// where group m begins, hist a workspace of perm_hist_bytes(B).
+size_t perm_hist_bytes(int32_t B);
+hipError_t launch_group_perm(int32_t B, const int32_t* seg_offsets, const int32_t* starts, int32_t* hist,
+                             int32_t* perm, hipStream_t stream);
+
 // Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,
                          const double* ED, const double* C, double dt, int yaw_mode,

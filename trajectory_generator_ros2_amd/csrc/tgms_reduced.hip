@@ -1660,6 +1660,75 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(Group
 }
 
 // ---------------------------------------------------------------------------
+// Grouping a ragged batch by M on the device (the refinement loop's plan, captured into
+// its graph): a stable counting sort of the trajectory ids by M = so[b+1] - so[b], the
+// same permutation the host planner builds (csrc/tgms_capi.hip upload_plan).  Blocks of
+// PERM_BLOCK trajectories; k_perm_hist counts each block's trajectories per M (wave
+// ballots), k_perm_scatter places them: the group's start + the counts of the blocks
+// before + the counts of the waves before + the lanes before.  M is validated on the host.
+constexpr int PERM_BLOCK = 1024;
+constexpr int PERM_BINS = 17;  // M = 1..16 (bin 0 unused)
+static_assert(PERM_BLOCK / W64 == PERM_BINS - 1, "k_perm_scatter: one wave per group");
+
+__device__ __forceinline__ int perm_m(const int32_t* __restrict__ so, int64_t b, int32_t B) {
+    return b < B ? (int)(so[b + 1] - so[b]) : 0;
+}
+
+__global__ __launch_bounds__(PERM_BLOCK) void k_perm_hist(int32_t B, const int32_t* __restrict__ so,
+                                                          int32_t* __restrict__ hist) {
+    __shared__ int32_t wc[PERM_BLOCK / W64][PERM_BINS];
+    const int t = threadIdx.x, w = t / W64, l = t % W64;
+    const int m = perm_m(so, (int64_t)blockIdx.x * PERM_BLOCK + t, B);
+#pragma unroll
+    for (int k = 1; k < PERM_BINS; ++k) {
+        const unsigned long long mask = __ballot(m == k);
+        if (l == 0) wc[w][k] = __popcll(mask);
+    }
+    __syncthreads();
+    if (t > 0 && t < PERM_BINS) {
+        int32_t s = 0;
+        for (int v = 0; v < PERM_BLOCK / W64; ++v) s += wc[v][t];
+        hist[(int64_t)blockIdx.x * PERM_BINS + t] = s;
+    }
+}
+
+struct PermStarts {
+    int32_t s[PERM_BINS];  // first index of group M in the permutation
+};
+
+__global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const int32_t* __restrict__ so,
+                                                             const int32_t* __restrict__ hist, PermStarts st,
+                                                             int32_t* __restrict__ perm) {
+    __shared__ int32_t wc[PERM_BLOCK / W64][PERM_BINS];
+    __shared__ int32_t base[PERM_BINS];
+    const int t = threadIdx.x, w = t / W64, l = t % W64;
+    const int64_t b = (int64_t)blockIdx.x * PERM_BLOCK + t;
+    const int m = perm_m(so, b, B);
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int k = 1; k < PERM_BINS; ++k) {
+        const unsigned long long mask = __ballot(m == k);
+        if (m == k) mine = mask;
+        if (l == 0) wc[w][k] = __popcll(mask);
+    }
+    {  // the blocks before this one: wave w sums group w + 1 over them, 64 blocks per step
+        const int g = w + 1;  // PERM_BLOCK / W64 == PERM_BINS - 1 waves, one per group
+        int32_t s = 0;
+        for (unsigned v = l; v < blockIdx.x; v += W64) s += hist[(int64_t)v * PERM_BINS + g];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if (l == 0) base[g] = st.s[g] + s;
+    }
+    __syncthreads();
+    if (m > 0) {
+        int32_t r = base[m];
+        for (int v = 0; v < w; ++v) r += wc[v][m];
+        r += __popcll(mine & ((1ull << l) - 1ull));
+        perm[r] = (int32_t)b;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Lane-per-trajectory solve of a uniform batch with an even number of segments
 // (configs 2-4: M = 10 is the headline).  One LANE owns one trajectory, 64 per
 // wavefront, one wavefront per SIMD: the 512-register budget holds the whole
@@ -2266,6 +2335,21 @@ hipError_t multi_launch(const GroupTable& tab, bool refine, const int32_t* so, c
 }
 
 }  // namespace
+
+size_t perm_hist_bytes(int32_t B) {
+    return (size_t)((B + PERM_BLOCK - 1) / PERM_BLOCK) * PERM_BINS * sizeof(int32_t);
+}
+
+hipError_t launch_group_perm(int32_t B, const int32_t* so, const int32_t* starts, int32_t* hist, int32_t* perm,
+                             hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((B + PERM_BLOCK - 1) / PERM_BLOCK);
+    PermStarts st{};
+    for (int m = 1; m < PERM_BINS; ++m) st.s[m] = starts[m];
+    TGMS_LAUNCH(k_perm_hist, dim3(grid), dim3(PERM_BLOCK), 0, stream, B, so, hist);
+    TGMS_LAUNCH(k_perm_scatter, dim3(grid), dim3(PERM_BLOCK), 0, stream, B, so, hist, st, perm);
+    return hipSuccess;
+}
 
 // (instantiated only for the classes a call can launch: end derivatives use the ED
 // boundary, so e.g. <1, TWO_WAVE_MAX_M, true> never exists)
