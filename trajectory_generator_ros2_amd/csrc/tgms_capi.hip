@@ -1698,7 +1698,10 @@ tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32
                                           const double* dW, double* dT, const double* dED, double k_T, double eta,
                                           int32_t iters, double* dC, double* d_cost, int32_t* dSt, void* stream) {
     if (!h) return TGMS_ERR_INVALID_ARG;
-    if (!h->multi)
+    // one device and no self-gather: the whole batch is device 0's shard, solved in place,
+    // so the single-device loop (its captured graph, the M grouping on the device) is that
+    // shard's path
+    if (!h->multi || (h->multi->n == 1 && !h->multi->self_gather))
         return tgms_refine_loop_device(h, B, h_so, d_so, dW, dT, dED, k_T, eta, iters, dC, d_cost, dSt, stream);
     h->last_error.clear();
     tgms_status s = check_refine_args(h, k_T, eta);
