@@ -1720,11 +1720,11 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const in
         if (l == 0) base[g] = st.s[g] + s;
     }
     __syncthreads();
-    if (m > 0) {
-        int32_t r = base[m];
+    if (m >= 1 && m < PERM_BINS) {  // (a device copy of the offsets that disagrees with the
+        int32_t r = base[m];         // host's, which validated them, must not write out of range)
         for (int v = 0; v < w; ++v) r += wc[v][m];
         r += __popcll(mine & ((1ull << l) - 1ull));
-        perm[r] = (int32_t)b;
+        if (r >= 0 && r < B) perm[r] = (int32_t)b;
     }
 }
 
