@@ -38,6 +38,15 @@ namespace {
 // solve while its state fits 256 registers without spilling (M <= 11), else one.
 #define TGMS_WAVES(M) ((M) <= TGMS_TWO_WAVE_MAX_M ? 2 : 1)
 // One-wave-per-SIMD kernels solve the three axes side by side (pair_solve_joint).
+// The axis-sequential lane-pair solve reads the next knot's waypoints and 1/T from the
+// LDS stage one step ahead (the per-step SCHED_FENCE otherwise exposes the LDS latency at
+// every step): config 5 0.477-0.488 -> 0.462-0.473 ms, uniform M = 3/5 -2-3 % (round 4).
+#ifndef TGMS_PAIR_PREFETCH
+#define TGMS_PAIR_PREFETCH 1
+#endif
+#ifndef TGMS_JOINT_PREFETCH
+#define TGMS_JOINT_PREFETCH 0
+#endif
 #ifndef TGMS_JOINT_AXES
 #define TGMS_JOINT_AXES 1
 #endif
@@ -501,6 +510,24 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
     }
 }
 
+// knot_rhs_axis from waypoint values already in registers (wm, wk, wn: knots k-1, k, k+1).
+template <bool HAS_ED>
+__device__ __forceinline__ void knot_rhs_vals(int k, double wm, double wk, double wn, const double (&pp)[8],
+                                              const double (&pn)[8], const double (&u0)[3], double (&y)[3]) {
+    const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
+    const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+    const double dp = wk - wm;
+    const double dn = wn - wk;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) y[d] = fp[d] * dp + fn[d] * dn;
+    if (HAS_ED && k == 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) y[d] -= (KSE[e][d] * pp[5 - d - e]) * u0[e];
+    }
+}
+
 // Coefficients of axis a of virtual segment e (knots e, e+1 with derivatives xs, xe).
 // ---------------------------------------------------------------------------
 // Time-allocation refinement: instead of storing a
@@ -604,10 +631,9 @@ __device__ __forceinline__ void emit_c(const OutCtx& o, const double (&c)[8], in
 }
 
 template <int M, class Out>
-__device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
-                                          const double (&xs)[3], const double (&xe)[3], bool has_r,
-                                          bool zero = false) {
-    const double ws = L.w(e, a), we = L.w(e + 1, a);
+__device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, double r, bool right, int e, int a,
+                                            const double (&xs)[3], const double (&xe)[3], bool has_r,
+                                            bool zero = false) {
     const double w0 = right ? we : ws, w1 = right ? ws : we;
     // the odd lane runs the segment backwards: physical start = virtual knot e+1, with P
     const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
@@ -615,7 +641,6 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
     // Hermite -> monomial in r = 1/T scaled variables (no T needed):
     //   c4 = r P4, c5 = r^2 P5, c6 = r^3 P6, c7 = r^4 P7 with P linear in
     //   D = (w1 - w0) r^3, V = v r^2, A = a r, J = j at both ends.
-    const double r = L.r(e);
     const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
     const double D = (w1 - w0) * r3;
     const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
@@ -646,6 +671,13 @@ __device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool 
             emit_c<M>(o, c, a, e, has_r);
         }
     }
+}
+
+template <int M, class Out>
+__device__ __forceinline__ void emit_axis(const Out& o, const LaneView& L, bool right, int e, int a,
+                                          const double (&xs)[3], const double (&xe)[3], bool has_r,
+                                          bool zero = false) {
+    emit_axis_v<M, Out>(o, L.w(e, a), L.w(e + 1, a), L.r(e), right, e, a, xs, xe, has_r, zero);
 }
 
 // `valid` is a bool, or a callable returning it that runs after the factorisation
@@ -688,14 +720,28 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
         {
             double pp[8];
             rpowers(L.r(0), pp);
+#if TGMS_PAIR_PREFETCH  // the next step's LDS values are read one step ahead
+            double rk = L.r(1), wm = L.w(0, a), wk = L.w(1, a), wn = L.w(2, a);
+#endif
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
                 SCHED_FENCE();
                 const int k = s + 1;
                 double pn[8];
-                rpowers(L.r(k), pn);
                 double y[3];
+#if TGMS_PAIR_PREFETCH
+                const double rk1 = (s + 1 < NS) ? L.r(k + 1) : 0.0;
+                const double wn1 = (s + 1 < NS) ? L.w(k + 2, a) : 0.0;
+                rpowers(rk, pn);
+                knot_rhs_vals<HAS_ED>(k, wm, wk, wn, pp, pn, u0, y);
+                rk = rk1;
+                wm = wk;
+                wk = wn;
+                wn = wn1;
+#else
+                rpowers(L.r(k), pn);
                 knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0, y);
+#endif
                 if (s >= 1) {
                     double B[3][3], v0, v1, v2;
                     coupling(pp, B);
@@ -760,16 +806,26 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
         // final (segment s+1 right after knot s): the two are independent, which
         // gives the scheduler a second dependency chain to interleave ----
         MARK(ax_back);
+#if TGMS_PAIR_PREFETCH  // segment s+1's waypoints and 1/T, read one step ahead
+        double w_lo = L.w(NS, a), w_hi = L.w(NS + 1, a), r_n = L.r(NS);
+#endif
 #pragma unroll
         for (int s = NS - 1; s >= 0; --s) {
             SCHED_FENCE();
             const bool at_end = (s == nl - 1);
             const bool inside = (s < nl - 1);
+#if TGMS_PAIR_PREFETCH
+            const double w_next = L.w(s, a), r_next = L.r(s);
+#endif
             if (s + 1 < NS) {
                 double B[3][3];
                 {
                     double pb[8];
+#if TGMS_PAIR_PREFETCH
+                    rpowers(r_n, pb);
+#else
                     rpowers(L.r(s + 1), pb);
+#endif
                     coupling(pb, B);
                 }
                 double b[3], x0, x1, x2;
@@ -784,11 +840,23 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #pragma unroll
                 for (int d = 0; d < 3; ++d) Y[s][d] = at_end ? xm[d] : Y[s][d];
             }
+#if TGMS_PAIR_PREFETCH
+            if (s + 1 < NE)
+                emit_axis_v<M, Out>(O, w_lo, w_hi, r_n, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR, !spd_pair);
+            w_hi = w_lo;
+            w_lo = w_next;
+            r_n = r_next;
+#else
             if (s + 1 < NE) emit_axis<M, Out>(O, L, right, s + 1, a, Y[s], Y[s + 1], s + 1 < nR, !spd_pair);
+#endif
         }
         MARK(ax_emit);
         SCHED_FENCE();
+#if TGMS_PAIR_PREFETCH
+        emit_axis_v<M, Out>(O, w_lo, w_hi, r_n, right, 0, a, u0, Y[0], 0 < nR, !spd_pair);
+#else
         emit_axis<M, Out>(O, L, right, 0, a, u0, Y[0], 0 < nR, !spd_pair);
+#endif
     }
     MARK(ax_end);
     const double fin_pair = fin + pair_swap(fin);
@@ -862,18 +930,39 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
     {
         double pp[8];
         rpowers(L.r(0), pp);
+#if TGMS_JOINT_PREFETCH
+        double rk = L.r(1), wm[3], wk[3], wn[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            wm[a] = L.w(0, a);
+            wk[a] = L.w(1, a);
+            wn[a] = L.w(2, a);
+        }
+#endif
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             SCHED_FENCE();
             const int k = s + 1;
             double pn[8];
+#if TGMS_JOINT_PREFETCH
+            const double rk1 = (s + 1 < NS) ? L.r(k + 1) : 0.0;
+            double wn1[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) wn1[a] = (s + 1 < NS) ? L.w(k + 2, a) : 0.0;
+            rpowers(rk, pn);
+#else
             rpowers(L.r(k), pn);
+#endif
             double B[3][3];
             if (s >= 1) coupling(pp, B);
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 double y[3];
+#if TGMS_JOINT_PREFETCH
+                knot_rhs_vals<HAS_ED>(k, wm[a], wk[a], wn[a], pp, pn, u0[a], y);
+#else
                 knot_rhs_axis<HAS_ED>(L, k, a, pp, pn, u0[a], y);
+#endif
                 if (s >= 1) {
                     double v0, v1, v2;
                     ldl3_solve(Fa.F[s - 1], Y[s - 1][a][0], Y[s - 1][a][1], Y[s - 1][a][2], v0, v1, v2);
@@ -886,6 +975,15 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
             pin33(Y[s]);
 #pragma unroll
             for (int q = 0; q < 8; ++q) pp[q] = pn[q];
+#if TGMS_JOINT_PREFETCH
+            rk = rk1;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                wm[a] = wk[a];
+                wk[a] = wn[a];
+                wn[a] = wn1[a];
+            }
+#endif
         }
     }
     SCHED_FENCE();
@@ -938,16 +1036,34 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
         }
     }
     // ---- back substitution, three axes per knot; segment s+1 emitted right after ----
+#if TGMS_JOINT_PREFETCH
+    double w_lo[3], w_hi[3], r_n = L.r(NS);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w_lo[a] = L.w(NS, a);
+        w_hi[a] = L.w(NS + 1, a);
+    }
+#endif
 #pragma unroll
     for (int s = NS - 1; s >= 0; --s) {
         SCHED_FENCE();
         const bool at_end = (s == nl - 1);
         const bool inside = (s < nl - 1);
+#if TGMS_JOINT_PREFETCH
+        double w_next[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) w_next[a] = L.w(s, a);
+        const double r_next = L.r(s);
+#endif
         if (s + 1 < NS) {
             double B[3][3];
             {
                 double pb[8];
+#if TGMS_JOINT_PREFETCH
+                rpowers(r_n, pb);
+#else
                 rpowers(L.r(s + 1), pb);
+#endif
                 coupling(pb, B);
             }
 #pragma unroll
@@ -972,12 +1088,30 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
         if (s + 1 < NE) {
 #pragma unroll
             for (int a = 0; a < 3; ++a)
+#if TGMS_JOINT_PREFETCH
+                emit_axis_v<M, Out>(O, w_lo[a], w_hi[a], r_n, right, s + 1, a, Y[s][a], Y[s + 1][a], s + 1 < nR,
+                                    !spd_pair);
+#else
                 emit_axis<M, Out>(O, L, right, s + 1, a, Y[s][a], Y[s + 1][a], s + 1 < nR, !spd_pair);
+#endif
         }
+#if TGMS_JOINT_PREFETCH
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            w_hi[a] = w_lo[a];
+            w_lo[a] = w_next[a];
+        }
+        r_n = r_next;
+#endif
     }
     SCHED_FENCE();
 #pragma unroll
-    for (int a = 0; a < 3; ++a) emit_axis<M, Out>(O, L, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+    for (int a = 0; a < 3; ++a)
+#if TGMS_JOINT_PREFETCH
+        emit_axis_v<M, Out>(O, w_lo[a], w_hi[a], r_n, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+#else
+        emit_axis<M, Out>(O, L, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+#endif
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
     if (!spd_pair) return TGMS_ERR_SINGULAR;
