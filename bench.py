@@ -47,6 +47,26 @@ def band_flops_per_traj(M: int) -> float:
     return N * (9 + 2 * 9 * 21) + N * 3 * 2 * 18
 
 
+def refine_flops_per_traj(M: int, iters: int = 10) -> float:
+    """Algorithmic FP64 flops of one config-5 call per trajectory: the
+    one-sided block LDL^T of DESIGN.md §2 over the M - 1 interior knots, three axes, counted
+    operation by operation (an FMA is 2 flops; a reciprocal 1), `iters` passes that end in the
+    cost and its T-derivative per segment-axis (seg_cost_p) plus the update, and one pass that
+    ends in the coefficients and the cost (seg_cost_q).  Per interior knot: powers 6, the
+    diagonal block 18, the coupling 9, G = S^-1 C 45 and the Schur update 36 (from the second
+    knot on), the 3x3 LDL^T 14; per knot and axis: right-hand side 11, forward 33, back 18.
+    Per segment and axis: the Hermite -> P4..P7 map 58, then cost + gradient 84, or the
+    coefficients 4 + cost 27; per segment the update 8.  This is what the algorithm needs,
+    not what the lane-pair kernels execute (their twisted interface and duplicated blocks
+    are in the executed count beside it)."""
+    nk = M - 1
+    fac = nk * (6 + 18 + 9 + 14) + max(nk - 1, 0) * (45 + 36)
+    sub = 3 * (nk * (11 + 18) + nk * 15 + max(nk - 1, 0) * 18)
+    grad_pass = fac + sub + M * 3 * (58 + 84) + M * 8
+    final_pass = fac + sub + M * 3 * (58 + 4 + 27)
+    return float(iters * grad_pass + final_pass)
+
+
 def dense_flops_per_traj(M: int) -> float:
     N = 14 * M + 2
     return 2.0 / 3.0 * N ** 3 + 6.0 * N ** 2
@@ -153,7 +173,7 @@ def cpu_baseline(B: int, M: int, target_s: float):
 
 
 C5_PMC_FILE = "profiles/c5_pmc.json"
-BYTE_MIX_FLOOR_US = 28.6  # config 3's byte mix with no compute, best occupancy (profiles/r03_runstore_occ.txt)
+BYTE_MIX_FLOOR_US = 28.6  # config 3's byte mix with no compute, best occupancy (profiles/archive/r03_runstore_occ.txt)
 
 
 def _c5_shard(so_all, W_all, T_all, bounds, part, dev):
@@ -202,6 +222,15 @@ def _c5_time(solver, sh, dev, stream, iters, k_T, eta, reps):
         call()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / reps * 1e3
+    host = []
+    for _ in range(reps):  # host time of one call (scan + graph replay), the GPU idle
+        dT.copy_(sh["T0"])
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        call()
+        host.append((time.perf_counter() - h0) * 1e3)
+        torch.cuda.synchronize()
+    _c5_time.host_ms = sorted(host)[reps // 2]
     return ms, wall, int((dst != 0).sum().item())
 
 
@@ -244,7 +273,8 @@ def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_
     nbytes = (Sg + B) * 24 + 2 * Sg * 8 + Sg * 192 + B * (8 + 4) + (B + 1) * 4
     line = {"workload": f"config5: shard {part} of 8 (cost-balanced, {B} trajectories) of a {B_total}-trajectory "
                         f"ragged batch, M~U{{2..16}}, {iters} refinement steps + final solve",
-            "ms_per_batch": ms, "ms_wall_per_call": wall, "trajectories_per_s": B / (ms * 1e-3), "segments": Sg,
+            "ms_per_batch": ms, "ms_wall_per_call": wall, "host_ms_per_call": getattr(_c5_time, "host_ms", None),
+            "trajectories_per_s": B / (ms * 1e-3), "segments": Sg,
             "k_T": k_T, "eta": eta,
             "timing": "median of single-call HIP event pairs on the launch stream; wall per call beside"}
     if shard_ms:
@@ -272,21 +302,30 @@ def config5_line(solver, dev, stream, world, rank, B_total=1048576, iters=10, k_
         w_all += waves * (2 + m_)
         w_live += waves * (2 + m_) * (2.0 * n_ / (64.0 * waves))
     lane_frac = w_live / w_all if w_all else 1.0
+    m_of = np.diff(sh["so"])
+    alg_flops = float(sum(refine_flops_per_traj(int(m_), iters) * int(c_)
+                          for m_, c_ in enumerate(np.bincount(m_of, minlength=17)) if m_ and c_))
+    tf_alg = alg_flops / (ms * 1e-3) / 1e12
     if pmc:
         tf = pmc["fp64_flops_per_call"] / (ms * 1e-3) / 1e12
         tf_lane = tf * lane_frac
-        line["roofline"] = {"bound": "fp64_valu", "achieved": tf_lane, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                            "frac": tf_lane / FP64_PEAK_TFS, "flops_per_call": pmc["fp64_flops_per_call"] * lane_frac,
+        line["roofline"] = {"bound": "fp64_valu", "achieved": tf_alg, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                            "frac": tf_alg / FP64_PEAK_TFS, "flops_per_call": alg_flops,
+                            "flops_definition": "algorithmic: bench.refine_flops_per_traj (the O(M) block LDL^T, "
+                                                "gradient and update, operation by operation) summed over the shard",
                             "lane_fraction": lane_frac,
+                            "executed_lane_accurate": {"achieved": tf_lane, "frac": tf_lane / FP64_PEAK_TFS,
+                                                       "flops_per_call": pmc["fp64_flops_per_call"] * lane_frac},
                             "executed": {"achieved": tf, "frac": tf / FP64_PEAK_TFS,
                                          "flops_per_call": pmc["fp64_flops_per_call"],
                                          "note": "every executed FP64 wave-instruction counted as 64 lanes"},
                             "flops_source": f"{C5_PMC_FILE} (executed FP64 flops, rocprofv3 --pmc of "
                                             f"scripts/c5bench.py: the same call), / this run's event time",
                             "valu_issue_frac": pmc["valu_insts_per_call"] * 4 / (1024 * 2.4e9 * ms * 1e-3),
-                            "hbm": hbm, "kernels": "k_refine_loop_multi<1,13> (two waves per SIMD) + <14,16> (one), concurrent"}
+                            "hbm": hbm, "kernels": "k_refine_loop_dev<1,13> (two waves per SIMD) + <14,16> (one), concurrent"}
     else:
-        line["roofline"] = {"bound": "fp64_valu", "achieved": None, "hbm": hbm}
+        line["roofline"] = {"bound": "fp64_valu", "achieved": tf_alg, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                            "frac": tf_alg / FP64_PEAK_TFS, "flops_per_call": alg_flops, "hbm": hbm}
     return line
 
 
@@ -458,6 +497,66 @@ def node_line(reps=20):
             "goals": n_goals, "ms_params_to_goals": gpu_ms,
             "ms_generate_traj_warm": sorted(tw)[reps // 2] * 1e3,
             "cpu_oracle_ms_solve_and_sample": sorted(tc)[reps // 2] * 1e3}
+
+
+def uniform_large_m_line(solver, dev, stream, Ms=(12, 14, 16), B=65536, sets=4, K=20):
+    """Uniform batches above the lane kernel's M range: 65,536
+    trajectories per launch, a fresh batch every launch (`sets` rotated, beyond the Infinity
+    Cache), HIP events around K launches; algorithmic bytes as the headline's.  Even M >= 12
+    run the joint lane-pair solve with whole-line output (k_reduced_uniform_lines)."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    out = {}
+    sp = stream.cuda_stream
+    for M in Ms:
+        bufs = []
+        for k in range(sets):
+            _, Wk, Tk = S.uniform_batch(B, M, seed=S.SEED + 1000 + k)
+            bufs.append((torch.from_numpy(Wk).to(dev), torch.from_numpy(Tk).to(dev),
+                         torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev)))
+        dS = torch.empty(B, dtype=torch.int32, device=dev)
+        for k in range(sets):
+            solver.solve_uniform_device(B, M, *bufs[k], dS, stream=sp)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(K):
+            solver.solve_uniform_device(B, M, *bufs[k % sets], dS, stream=sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+        us = e0.elapsed_time(e1) / K * 1e3
+        nbytes = algorithmic_bytes_per_traj(M) * B
+        kern = (f"k_lane_uniform<{M}>" if M % 2 == 0 and M <= 10 else
+                f"k_reduced_uniform_lines<{M}>" if M % 2 == 0 else f"k_reduced_uniform<{M}>")
+        out[f"M{M}"] = {"us_per_launch": us, "algorithmic_bytes": nbytes, "GBs": nbytes / (us * 1e-6) / 1e9,
+                        "frac": nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "kernel": kern}
+        del bufs
+        torch.cuda.empty_cache()
+    out["workload"] = f"uniform {B} x M in {list(Ms)}, fresh batch every launch ({sets} rotated), events over {K}"
+    return out
+
+
+def host_backend_node_line(reps=20):
+    """Config 1 as BASELINE.json states it, "ROS2 node up, no GPU": the node's MinSnap
+    primitive on the explicit host backend (`minsnap_backend: host`, tgms_create_host) --
+    readParameters (validation + solve, B = 1) and generateTraj (sample + append) on this
+    CPU thread, as the reference generates on its executor thread."""
+    from trajectory_generator_ros2_amd.node import MinSnapNode
+    wp = [0.0, 0.0, 1.0, 2.0, 1.0, 1.5, 3.0, -1.0, 2.0, 0.5, -2.0, 1.0]
+    params = {"alt": 1.8, "pub_freq": 100.0, "traj_type": "MinSnap", "waypoints": wp, "seg_times": [2.0, 2.0, 2.5],
+              "yaw_mode": "constant", "yaw": 0.0, "stop_accel": 1.0, "x_min": -5.0, "x_max": 5.0,
+              "y_min": -5.0, "y_max": 5.0, "z_min": -5.0, "z_max": 5.0, "minsnap_backend": "host"}
+    ts, n_goals = [], 0
+    for _ in range(reps + 2):
+        t0 = time.perf_counter()
+        n = MinSnapNode(params)
+        assert n.read_parameters()
+        n_goals = n.generate_traj()
+        ts.append(time.perf_counter() - t0)
+        n.close()
+    return {"workload": "config1 on the host backend (no GPU used): 1 goal, 4 waypoints, 3 segments, 100 Hz",
+            "goals": n_goals, "ms_params_to_goals": sorted(ts[2:])[reps // 2] * 1e3, "cores": 1}
 
 
 def host_line(solver, B, M, W, T, reps=20):
@@ -693,16 +792,21 @@ def config5_full_line(devs, reps=3, B_total=1048576, iters=10, k_T=1.0, eta=0.1)
                 mh.refine_loop_multi_device(so, dso, dW, dT, k_T, eta, iters, dC, dcost, dst,
                                             stream=stream.cuda_stream)
             wall, _ = _timed_multi(run, stream, reps, devs)
-            # events around the call alone
+            # events around the call alone; the host time of the call (offsets scan, shard
+            # plan, graph replays, RCCL groups) with every device idle
             run()
             torch.cuda.synchronize(0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            evs = []
+            evs, host = [], []
             for _ in range(reps):
                 dT.copy_(T0)
+                for dd in devs:
+                    torch.cuda.synchronize(dd)
                 e0.record(stream)
+                h0 = time.perf_counter()
                 mh.refine_loop_multi_device(so, dso, dW, dT, k_T, eta, iters, dC, dcost, dst,
                                             stream=stream.cuda_stream)
+                host.append((time.perf_counter() - h0) * 1e3)
                 e1.record(stream)
                 torch.cuda.synchronize(0)
                 evs.append(e0.elapsed_time(e1))
@@ -715,6 +819,7 @@ def config5_full_line(devs, reps=3, B_total=1048576, iters=10, k_T=1.0, eta=0.1)
                         f"refinement steps + final solve in one tgms_refine_loop_multi_device call over {n} "
                         f"device(s)",
             "devices": n, "ms_per_call": ms, "ms_per_call_wall_incl_time_reset": wall,
+            "host_ms_per_call": sorted(host)[len(host) // 2],
             "trajectories_per_s": B / (ms * 1e-3), "segments": Sg, "k_T": k_T, "eta": eta,
             "status_failures": bad, "costs_finite": finite}
 
@@ -776,6 +881,8 @@ def main():
                          "library's multi-GPU call, or a per-rank RCCL gather under a launcher): 1/0")
     ap.add_argument("--node-line", type=int, default=1, help="config-1 node-path latency side line: 1/0")
     ap.add_argument("--host-line", type=int, default=1, help="PCIe-inclusive host-buffer side line: 1/0")
+    ap.add_argument("--uniform-large-m", type=int, default=1,
+                    help="uniform M = 12/14/16 side line (fresh batches): 1/0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0: skip the CPU baseline")
     ap.add_argument("--full-lines-only", action="store_true",
                     help="internal: print only the config4_full / config5_full lines over devices 0..N-1 (the "
@@ -978,13 +1085,18 @@ def main():
     if args.sample_traj > 0:
         sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
 
+    uniform_m = None
+    if args.uniform_large_m and args.method == "reduced":
+        uniform_m = _side("uniform_large_m", lambda: uniform_large_m_line(solver, dev, stream))
+
     host = None
     if args.host_line and rank == 0:
         host = host_line(solver, B, M, W, T)
 
-    node = None
+    node = node_host = None
     if args.node_line and rank == 0:
         node = node_line()
+        node_host = _side("node_config1_host_backend", host_backend_node_line)
 
     # rank-0-only host work, after every GPU timing (the other ranks wait at the
     # final barrier)
@@ -1034,11 +1146,11 @@ def main():
                          "launch_ms": launch_ms_max,
                          # the measured floor of this byte mix with NO compute (read the inputs,
                          # write the coefficients, fresh buffers, best occupancy and rounds:
-                         # scripts/micro/occstore.hip, profiles/r03_runstore_occ.txt): the
+                         # scripts/micro/occstore.hip, profiles/archive/r03_runstore_occ.txt): the
                          # fraction of the attainable rate the kernel reaches
                          "floor_us": BYTE_MIX_FLOOR_US if (B, M) == (65536, 10) else None,
                          "floor_frac": (BYTE_MIX_FLOOR_US / (launch_ms_max * 1e3)) if (B, M) == (65536, 10) else None,
-                         "floor_source": "profiles/r03_runstore_occ.txt (reads + stores, no compute, 2 waves/SIMD, "
+                         "floor_source": "profiles/archive/r03_runstore_occ.txt (reads + stores, no compute, 2 waves/SIMD, "
                                          "4 rounds: 28.6 us for 22.5 MB read + 126 MB written)",
                          "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
                          "algorithmic_bytes_per_launch": bpl},
@@ -1052,8 +1164,10 @@ def main():
             "config4_full": config4_full,
             "config5": config5,
             "config5_full": config5_full,
+            "uniform_large_m": uniform_m,
             "host_path": host,
             "node_config1": node,
+            "node_config1_host_backend": node_host,
         }
         if capture_error is not None:
             line["config"]["graph_capture_error"] = capture_error

@@ -42,7 +42,8 @@
  *     tgms_refine_loop_device, the multi-GPU calls, a band capture with no slab large
  *     enough) return TGMS_ERR_UNSUPPORTED while their stream is capturing;
  *   - there is no CPU fallback: with no usable GPU, tgms_create fails with
- *     TGMS_ERR_NO_DEVICE.
+ *     TGMS_ERR_NO_DEVICE.  A GPU-less node asks for the host backend explicitly
+ *     (tgms_create_host: solve + sample on the CPU, config 1).
  *
  * Layouts (fp64, row-major, trajectory-major).  A batch is CSR over segments:
  * trajectory b has M_b = seg_offsets[b+1] - seg_offsets[b] segments (1..TGMS_MAX_SEGMENTS):
@@ -63,7 +64,7 @@
 extern "C" {
 #endif
 
-#define TGMS_ABI_VERSION 1
+#define TGMS_ABI_VERSION 2 /* 2: tgms_piece.ws_off gained the device plan regions (round 5) */
 #define TGMS_MAX_SEGMENTS 16       /* reduced-Hessian kernel: M = 1..16 (config 5 range) */
 #define TGMS_DENSE_MAX_SEGMENTS 10 /* dense KKT kernel: N = 14M+2 <= 142 (+3 right-hand sides) fits a 256-thread workgroup's registers */
 #define TGMS_GOAL_STRIDE 14        /* doubles per sample: p[3] v[3] a[3] j[3] psi dpsi */
@@ -104,6 +105,12 @@ const char* tgms_status_string(int status);
 
 /* Create a handle on HIP device `device` (ordinal).  TGMS_ERR_NO_DEVICE if none. */
 tgms_status tgms_create(tgms_handle** out, int device);
+/* The explicit host backend (BASELINE config 1: a ROS 2 node with no GPU; the reference
+ * generates on the executor thread's CPU, src/TrajectoryGenerator.cpp:54-57, :71).  A host
+ * handle runs tgms_solve_batch (reduced method) and tgms_sample_batch on the calling thread
+ * with the GPU path's conventions; every other entry point returns TGMS_ERR_UNSUPPORTED on
+ * it.  Chosen by the caller only: tgms_create never falls back to it. */
+tgms_status tgms_create_host(tgms_handle** out);
 void tgms_destroy(tgms_handle* h);
 /* Last error text of this handle ("" if none).  Valid until the next call. */
 const char* tgms_last_error(const tgms_handle* h);
@@ -121,7 +128,14 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M,
                                       const double* d_end_derivs, double* d_coeffs,
                                       int32_t* d_status, void* stream);
 /* Ragged batch (config 5).  h_seg_offsets is a host copy used to plan the launch
- * (trajectories are grouped by M so every wavefront runs one M). */
+ * (trajectories are grouped by M so every wavefront runs one M).  The refinement loops
+ * group the batch on the device from d_seg_offsets, which must hold the same values as
+ * h_seg_offsets: tgms_refine_loop_device reads h_seg_offsets once (validation, uniform
+ * detection); tgms_refine_loop_multi_device reads only seg_offsets[0], [B] and the shard
+ * and piece cuts (binary search), so per-trajectory M is checked on the devices alone.
+ * Device offsets with an M outside 1..16 or another span run nothing in the shard piece
+ * that holds them and mark its trajectories TGMS_ERR_INVALID_ARG in d_status, with zero
+ * coefficients and costs and the times kept; the call itself returns TGMS_OK. */
 tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
                                     const int32_t* d_seg_offsets, const double* d_waypoints,
                                     const double* d_seg_times, const double* d_end_derivs,
@@ -194,7 +208,7 @@ tgms_status tgms_sample_batch_device(tgms_handle* h, int32_t B, const int32_t* d
  * in the reference, whose caller (TrajectoryGenerator.hpp:83, src/TrajectoryGenerator.cpp:71)
  * holds one Trajectory; this is the swarm / sampling planner's batch path (configs 4, 5). */
 tgms_status tgms_create_multi(tgms_handle** out, int device_count);
-int tgms_device_count(const tgms_handle* h); /* 1 for a tgms_create handle */
+int tgms_device_count(const tgms_handle* h); /* 1 for a tgms_create handle, 0 for a host handle */
 /* Host-only shard planner: bounds [parts+1] of contiguous trajectory ranges with
  * ~equal cost (reduced / band: 2 + M_b, dense KKT: (14 M_b + 2)^3 per trajectory). */
 tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t parts, int method,
@@ -208,7 +222,9 @@ tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t part
  * device, device 0 -> dev), then gather groups 4..7 (piece k's results, dev -> device 0);
  * each transfer is one ncclSend on one side and one ncclRecv on the other.  flags:
  * TGMS_SCHED_* below.  Returns TGMS_ERR_INVALID_ARG (with *n_pieces / *n_xfers set to the
- * sizes needed) when piece_cap or xfer_cap is too small. */
+ * sizes needed) when piece_cap or xfer_cap is too small.  With TGMS_SCHED_REFINE it does
+ * exactly the host work of tgms_refine_loop_multi_device before its first transfer (no pass
+ * over the offsets; the cuts checked); without, the solve's validation pass as well. */
 #define TGMS_SCHED_REFINE 1
 #define TGMS_SCHED_END_DERIVS 2
 #define TGMS_SCHED_COEFFS 4
@@ -218,11 +234,15 @@ tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t part
 typedef struct tgms_piece {
     int32_t dev, piece, lo, hi; /* trajectories [lo, hi) */
     int64_t s0, s1;             /* segments [s0, s1) */
-    int64_t ws_off[9];          /* byte offsets: rebased seg_offsets, permutation, W, T, T2, ED, C, status, cost */
+    int64_t ws_off[11];         /* byte offsets: seg_offsets (ragged: rebased for a solve, the raw slice
+                                   for a refinement loop), permutation, W, T, T2, ED, C, status, cost,
+                                   and for a ragged refinement loop the device grouping's block counts
+                                   and its device-side plan (uniform batches: empty regions) */
 } tgms_piece;
 typedef struct tgms_xfer {
     int32_t dev, piece, gather; /* gather 0: device 0 -> dev (scatter), 1: dev -> device 0 */
-    int32_t array;              /* 0 W, 1 T, 2 end derivs, 3 coeffs, 4 status, 5 cost */
+    int32_t array;              /* 0 W, 1 T, 2 end derivs, 3 coeffs, 4 status, 5 cost, 6 seg_offsets
+                                   (the slice [lo, hi] of a ragged refinement loop's piece) */
     int64_t batch_elem;         /* element offset in the device-0 batch array */
     int64_t ws_byte;            /* byte offset in dev's piece workspace */
     int64_t count;              /* elements */
@@ -243,7 +263,9 @@ tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32
                                           const double* d_seg_times, const double* d_end_derivs,
                                           double* d_coeffs, int32_t* d_status, void* stream);
 /* tgms_refine_loop_device over the devices (config 5): times (in place), costs,
- * coefficients and statuses gathered back to device 0. */
+ * coefficients and statuses gathered back to device 0.  Every batch (uniform ones too) runs
+ * the device-grouped loop; the host does no pass over the offsets (see
+ * tgms_solve_batch_device above: a piece with bad offsets fails on its device). */
 tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
                                           const int32_t* d_seg_offsets, const double* d_waypoints,
                                           double* d_seg_times, const double* d_end_derivs, double k_T,

@@ -527,6 +527,25 @@ int oracle_refine_times(int formulation, int M, const double* W, double* T, cons
     return ORACLE_OK;
 }
 
+/* One step's ingredients at fixed times: the per-segment gradient dJ_i/dT_i and
+ * F = sum_i J_i + kT sum_i T_i (what oracle_refine_times feeds its update), so a test
+ * can pin a single GPU step, gradient included, without the iteration's amplification. */
+int oracle_refine_grad(int formulation, int M, const double* W, const double* T, const double* ED, double kT,
+                       double* dJ, double* cost) {
+    double c[24 * ORACLE_MAX_SEGMENTS];
+    if (!W || !T || !dJ || M < 1 || M > ORACLE_MAX_SEGMENTS || !inputs_valid(M, W, T, ED)) return ORACLE_INVALID;
+    const int st = oracle_solve(formulation, M, W, T, ED, c);
+    if (st != ORACLE_OK) return st;
+    double F = 0.0;
+    for (int i = 0; i < M; ++i) {
+        double J;
+        segment_cost(c + 24 * i, W + 3 * i, W + 3 * (i + 1), T[i], &J, &dJ[i]);
+        F += J + kT * T[i];
+    }
+    if (cost) *cost = F;
+    return ORACLE_OK;
+}
+
 int oracle_refine_batch(int formulation, int32_t B, const int32_t* seg_offsets, const double* waypoints,
                         double* seg_times, const double* end_derivs, double kT, double eta, int iters,
                         double* cost, double* coeffs, int32_t* status, int nthreads) {

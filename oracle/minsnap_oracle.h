@@ -86,6 +86,10 @@ int64_t oracle_sample_count(double total_T, double dt);
 int oracle_refine_times(int formulation, int M, const double* waypoints, double* seg_times,
                         const double* end_derivs, double kT, double eta, int iters, double* cost,
                         double* coeffs);
+/* The per-segment gradient dJ_i/dT_i (dJ[M]) and F at the given times (one solve, no
+ * update): the ingredients of one refinement step. */
+int oracle_refine_grad(int formulation, int M, const double* waypoints, const double* seg_times,
+                       const double* end_derivs, double kT, double* dJ, double* cost);
 int oracle_refine_batch(int formulation, int32_t B, const int32_t* seg_offsets, const double* waypoints,
                         double* seg_times, const double* end_derivs, double kT, double eta, int iters,
                         double* cost, double* coeffs, int32_t* status, int nthreads);

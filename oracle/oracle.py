@@ -55,6 +55,8 @@ def lib():
         L.oracle_refine_batch.argtypes = [ctypes.c_int, ctypes.c_int32, ip, dp, dp, dp, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_int, dp, dp, ip, ctypes.c_int]
         L.oracle_refine_batch.restype = ctypes.c_int
+        L.oracle_refine_grad.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, ctypes.c_double, dp, dp]
+        L.oracle_refine_grad.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -139,6 +141,18 @@ def refine_times(waypoints, seg_times, end_derivs=None, k_T=1.0, eta=0.1, iters=
     st = lib().oracle_refine_times(formulation, M, _dp(W), _dp(T), _dp(ED), float(k_T), float(eta), int(iters),
                                    _dp(cost), _dp(C))
     return T, float(cost[0]), C, st
+
+
+def refine_grad(waypoints, seg_times, end_derivs=None, k_T=1.0, formulation: int = REDUCED):
+    """One trajectory at fixed times: (dJ_i/dT_i [M], F = sum J + k_T sum T, status) — the
+    ingredients of one refinement step (oracle_refine_grad)."""
+    W = np.ascontiguousarray(waypoints, dtype=np.float64)
+    T = np.ascontiguousarray(seg_times, dtype=np.float64)
+    ED = None if end_derivs is None else np.ascontiguousarray(end_derivs, dtype=np.float64)
+    dJ = np.zeros(T.shape[0])
+    cost = np.zeros(1)
+    st = lib().oracle_refine_grad(formulation, T.shape[0], _dp(W), _dp(T), _dp(ED), float(k_T), _dp(dJ), _dp(cost))
+    return dJ, float(cost[0]), st
 
 
 def refine_batch(seg_offsets, waypoints, seg_times, end_derivs=None, k_T=1.0, eta=0.1, iters=10,

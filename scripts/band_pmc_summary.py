@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch means of the band-KKT kernel's counters over scripts/gpu_bandpmc.sh's passes
+"""Per-launch means of the band-KKT kernel's counters over the `pmcs` passes of scripts/session.sh (scripts/bandbench.py)
 (one counter group per rocprofv3 --pmc run) plus the kernel-trace mean duration.
 usage: band_pmc_summary.py [gpurun_out/bandpmc] [header line]"""
 import collections, csv, glob, os, sys

@@ -13,10 +13,11 @@ os.makedirs(vdir, exist_ok=True)
 srcs = src.split(",")  # several sources: comma-separated
 vobjs = []
 for sname in srcs:
-    obj = os.path.join(B.OBJDIR, "variant_%s_%s.o" % (name, sname))
+    obj = os.path.join(B.OBJDIR, "variant_%s_%s.o" % (name, os.path.basename(sname)))
     B._run([B.HIPCC] + B.HIP_FLAGS + flags + ["-c", os.path.join(B.CSRC, sname), "-o", obj])
     vobjs.append(obj)
-objs = [os.path.join(B.OBJDIR, s + ".o") for s in B.HIP_SOURCES + B.CXX_SOURCES if s not in srcs] + vobjs
+bases = [os.path.basename(s) for s in srcs]  # (a source may be an absolute path: a saved older version)
+objs = [os.path.join(B.OBJDIR, s + ".o") for s in B.HIP_SOURCES + B.CXX_SOURCES if s not in bases] + vobjs
 out = os.path.join(vdir, "libtgms_%s.so" % name)
 B._run([B.HIPCC, "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o", out] + objs + ["-ldl"])
 print(out)

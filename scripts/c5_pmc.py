@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold the config-5 PMC passes (scripts/gpu_r03d.sh: rocprofv3 --pmc of scripts/c5bench.py)
+"""Fold the config-5 PMC passes (scripts/session.sh `pmcs` step: rocprofv3 --pmc of scripts/c5bench.py)
 into profiles/c5_pmc.json: per tgms_refine_loop_device call of bench.py's config-5
 share, the executed FP64 flops (64 lanes x (ADD + MUL + 2 FMA)), VALU instructions and
 HBM bytes (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE, MI355X_MICROARCH.md), summed over

@@ -309,6 +309,95 @@ def test_refine_matches_oracle(solver, oracle, ragged):
     assert not np.array_equal(Tg, T)
 
 
+def _step_gradient_from_coeffs(C, W, T, ED, kT):
+    """The refinement step's gradient formula (csrc/tgms_reduced.hip seg_cost_p: the snap
+    cost's T-derivative from the scaled monomial data P4..P7, r = 1/T) evaluated in numpy on
+    a solve's own knot data: segment i's start (v, a, j) from its coefficients, its end data
+    from the next segment's start (the shared knot) or the final end derivatives."""
+    M = T.shape[0]
+    out = np.zeros(M)
+    for i in range(M):
+        r = 1.0 / T[i]
+        r2, r3 = r * r, r * r * r
+        for a in range(3):
+            c = C[i, a]
+            v0, a0, j0 = c[1], 2.0 * c[2], 6.0 * c[3]
+            if i + 1 < M:
+                cn = C[i + 1, a]
+                v1, a1 = cn[1], 2.0 * cn[2]
+            else:
+                v1, a1 = (ED[9 + a], ED[12 + a]) if ED is not None else (0.0, 0.0)
+            D = (W[i + 1, a] - W[i, a]) * r3
+            V0, A0, V1, A1 = v0 * r2, a0 * r, v1 * r2, a1 * r
+            P = [c[4] / r, c[5] / r2, c[6] / r3, c[7] / (r2 * r2)]
+            Qv = [105.0 * D - 40.0 * V0 - 5.0 * A0 - 30.0 * V1 + 2.5 * A1,
+                  -252.0 * D + 90.0 * V0 + 10.0 * A0 + 78.0 * V1 - 7.0 * A1,
+                  210.0 * D - 72.0 * V0 - 7.5 * A0 - 68.0 * V1 + 6.5 * A1,
+                  -60.0 * D + 20.0 * V0 + 2.0 * A0 + 20.0 * V1 - 2.0 * A1]
+            Hm = np.array([[576.0, 1440.0, 2880.0, 5040.0], [1440.0, 4800.0, 10800.0, 20160.0],
+                           [2880.0, 10800.0, 25920.0, 50400.0], [5040.0, 20160.0, 50400.0, 100800.0]])
+            HP = Hm @ np.array(P)
+            Q = float(np.dot(P, HP))
+            G = float(np.dot(Qv, HP))
+            out[i] += r2 * -(Q + 2.0 * G)
+    return out
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+@pytest.mark.parametrize("with_ed", [False, True])
+def test_refine_one_step_at_north_star_tolerance(solver, oracle, ragged, with_ed):
+    """ONE refinement step (iters = 1) against the oracle at north_star's 1e-9 with no
+    iteration to amplify rounding: the new times T_1, the cost at the input times (iters = 0)
+    and at T_1, the coefficients at T_1, each norm-wise per trajectory.  The per-segment
+    gradient dJ_i/dT_i the step applied, recovered from T_1 = T_0 exp(-eta T_0 (dJ + k_T) / F)
+    (unclamped segments), is held
+      - at 1e-9 to the step's formula evaluated in numpy on the GPU's own solve at T_0: the
+        step is exactly its formula on its solve;
+      - at 1e-6 to the oracle's gradient (oracle.refine_grad): the gradient is a difference of
+        large quadratic terms in the knot data, so rounding in the knot data of ANY fp64 solve
+        carries into it amplified.  The formula on the oracle's own coefficients disagrees with
+        the oracle's gradient by 1.5e-8 (no end derivatives) / 3.7e-8 (with), the host backend's
+        CPU solve by the same; the GPU's measured 1.6e-8 / 3.5e-7 (round 5; the same formula on
+        exact knot data agrees with the exact gradient to 2e-13).
+    Uniform batches run the step kernels, ragged ones the fused loop."""
+    from trajectory_generator_ros2_amd import synthetic as S
+    if ragged:
+        so, W, T = S.ragged_batch(257, 1, 16, seed=61)
+    else:
+        so, W, T = S.uniform_batch(257, 10, seed=62)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+    B = len(so) - 1
+    ED = np.random.default_rng(63).normal(scale=0.3, size=(B, 18)) if with_ed else None
+    kT, eta = 1.0, 0.02
+    _, C0, F0, st0, w0 = solver.refine(so, W, T, ED, kT, eta, 0)
+    T1, C1, F1, st1, w1 = solver.refine(so, W, T, ED, kT, eta, 1)
+    assert w0 == 0 and w1 == 0 and (st0 == 0).all() and (st1 == 0).all()
+    To, Fo, Co, sto = oracle.refine_batch(so, W, T, ED, kT, eta, 1, oracle.REDUCED)
+    assert (sto == 0).all()
+    assert np.abs(T1 / To - 1).max() <= TOL
+    assert np.abs(F1 / Fo - 1).max() <= TOL
+    assert batch_rel_err(so, C1, Co) <= TOL
+    worst_self, worst_or, worst_f0, used = 0.0, 0.0, 0.0, 0
+    for b in range(B):
+        s0, s1 = int(so[b]), int(so[b + 1])
+        Wb, Tb, EDb = W[s0 + b:s1 + b + 1], T[s0:s1], None if ED is None else ED[b]
+        dJ, Fr, st = oracle.refine_grad(Wb, Tb, EDb, kT, oracle.REDUCED)
+        assert st == 0
+        worst_f0 = max(worst_f0, abs(F0[b] / Fr - 1))
+        dtau = np.log(T1[s0:s1] / Tb)
+        free = np.abs(dtau) < 0.499  # the step clamps |dtau| at 1/2
+        g = -dtau * F0[b] / (eta * Tb) - kT
+        if free.any():
+            used += int(free.sum())
+            mine = _step_gradient_from_coeffs(C0[s0:s1], Wb, Tb, EDb, kT)
+            worst_self = max(worst_self, np.abs(g - mine)[free].max() / max(np.abs(mine).max(), 1e-300))
+            worst_or = max(worst_or, np.abs(g - dJ)[free].max() / max(np.abs(dJ).max(), 1e-300))
+    assert worst_f0 <= TOL
+    assert used >= 0.9 * len(T)
+    assert worst_self <= TOL, worst_self
+    assert worst_or <= 1e-6, worst_or
+
+
 def test_refine_device_step_and_errors(solver):
     import torch
     from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_UNSUPPORTED, METHOD_DENSE_KKT, TgmsError

@@ -50,12 +50,17 @@ FLAGS = [SOLVE, SOLVE | S.SCHED_END_DERIVS, SOLVE | S.SCHED_SELF_GATHER, REFINE,
          S.SCHED_STATUS]
 
 
-def _region_sizes(p, flags):
+def _region_sizes(p, flags, ragged):
+    """Bytes of ws_off[0..10]: offsets, permutation (ragged only), W, T, T2, ED, C, status,
+    cost, and for a refinement loop the device grouping's block counts and plan (round 5: every
+    refinement batch, uniform ones too, is grouped on the device, laid out as a ragged one)."""
     n, Sg = p["hi"] - p["lo"], p["s1"] - p["s0"]
     refine = bool(flags & S.SCHED_REFINE)
-    return [4 * (n + 1), 4 * n, 8 * 3 * (Sg + n), 8 * Sg, 8 * Sg if refine else 0,
+    dev = refine
+    ragged = ragged or refine
+    return [4 * (n + 1) if ragged else 0, 4 * n if ragged else 0, 8 * 3 * (Sg + n), 8 * Sg, 8 * Sg if refine else 0,
             8 * 18 * n if flags & S.SCHED_END_DERIVS else 0, 8 * 24 * Sg if flags & S.SCHED_COEFFS else 0,
-            4 * n, 8 * n if refine else 0]
+            4 * n, 8 * n if refine else 0, 17 * 4 * ((n + 1023) // 1024) if dev else 0, 1024 if dev else 0]
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
@@ -64,6 +69,7 @@ def test_schedule_structure(lib, n, flags):
     from trajectory_generator_ros2_amd.solver import multi_schedule, plan_shards
     for name, so in _batches().items():
         so = so.astype(np.int64)
+        ragged = len(set(np.diff(so).tolist())) > 1
         bounds, ws, P, X = multi_schedule(so, n, 0, flags)
         np.testing.assert_array_equal(bounds, plan_shards(so, n, 0))
         self_gather = bool(flags & S.SCHED_SELF_GATHER)
@@ -84,7 +90,7 @@ def test_schedule_structure(lib, n, flags):
             # workspace regions: aligned, inside, disjoint
             regs = []
             for p in mine:
-                for off, size in zip(p["ws_off"], _region_sizes(p, flags)):
+                for off, size in zip(p["ws_off"], _region_sizes(p, flags, ragged)):
                     assert off % ALIGN == 0
                     if size:
                         assert off + size <= ws[d], (name, d)
@@ -108,6 +114,7 @@ def test_schedule_structure(lib, n, flags):
                 3: (1, p["s0"] * 24, Sg * 24, 8, 6),
                 4: (1, p["lo"], npc, 4, 7),
                 5: (1, p["lo"], npc, 8, 8),
+                6: (0, p["lo"], npc + 1, 4, 0),
             }[x["array"]]
             assert (x["gather"], x["batch_elem"], x["count"], x["elem_bytes"], x["ws_byte"]) == \
                 (exp[0], exp[1], exp[2], exp[3], p["ws_off"][exp[4]]), (name, x)
@@ -119,6 +126,7 @@ def test_schedule_structure(lib, n, flags):
             want += [(1, 4)] if flags & S.SCHED_STATUS else []
             if flags & S.SCHED_REFINE:
                 want += [(1, 1), (1, 5)] if flags & S.SCHED_COST else [(1, 1)]
+                want += [(0, 6)]  # the offsets slice, planned on the device (uniform batches too)
             assert arrs == sorted(want), (name, arrs)
 
 
@@ -197,3 +205,84 @@ def test_schedule_arguments(lib):
         with pytest.raises(TgmsError) as e:
             multi_schedule(so, n, 0, SOLVE)
         assert e.value.status == ERR_INVALID_ARG
+
+
+def test_refine_schedule_leaves_per_trajectory_checks_to_the_devices(lib):
+    """Round 5: the refinement loop's host work reads only the cuts.  A bad M strictly
+    inside a piece passes the host (its device's k_group_plan rejects that piece:
+    tests/test_gpu_multi.py::test_refine_multi_bad_offsets_fail_on_the_device); offsets
+    whose shard or piece spans no M in 1..16 can give (the workspaces are sized from them) are
+    refused; a decrease that the cuts do not expose is again the devices' to reject."""
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, TgmsError
+    from trajectory_generator_ros2_amd import synthetic as SY
+    from trajectory_generator_ros2_amd.solver import multi_schedule
+    so = SY.ragged_batch(4000, 2, 16, seed=9)[0].astype(np.int32)
+    bad = so.copy()
+    bad[1001:] += 20  # trajectory 1000 gets M + 20
+    with pytest.raises(TgmsError):
+        multi_schedule(bad, 4, 0, SOLVE)
+    b, _, P, _ = multi_schedule(bad, 4, 0, REFINE)
+    assert not any(p["lo"] == 1000 or p["hi"] == 1001 for p in P)  # strictly inside a piece
+    for so_dec in ([0, 2, 4, 6, 3, 10, 12, 14, 16], [0, 2, 4, 1, 8, 10, 12, 14, 16]):
+        b, _, P, _ = multi_schedule(np.array(so_dec, np.int32), 4, 0, REFINE)
+        for q in P:
+            assert q["hi"] - q["lo"] <= q["s1"] - q["s0"] <= 16 * (q["hi"] - q["lo"])
+    for so_bad in ([0, 3, 100], [0, 3, 3], [0, 2, 4, 6, 8, 10, 12, 14, 9]):
+        with pytest.raises(TgmsError) as e:
+            multi_schedule(np.array(so_bad, np.int32), 4, 0, REFINE)
+        assert e.value.status == ERR_INVALID_ARG
+
+
+def test_shard_cuts_by_binary_search_match_the_prefix_sum_rule():
+    """Round 5: the reduced / band planner cuts ragged batches by binary search over the
+    integer running cost 2 (b + 1) + so[b + 1] (no pass over the batch), and the pieces of a
+    shard from the shard's own offsets slice; both must give shard.ragged_bounds' cuts."""
+    from trajectory_generator_ros2_amd import shard as SH
+    from trajectory_generator_ros2_amd import synthetic as SY
+    from trajectory_generator_ros2_amd.solver import multi_schedule, plan_shards
+    for seed, (B, lo, hi) in enumerate([(1, 1, 16), (7, 2, 16), (5000, 2, 16), (4096, 1, 3), (333, 15, 16)]):
+        so = SY.ragged_batch(B, lo, hi, seed=seed)[0].astype(np.int64)
+        for parts in (1, 2, 3, 4, 8, 13):
+            np.testing.assert_array_equal(plan_shards(so, parts, 0), SH.ragged_bounds(so, parts))
+        _, _, P, _ = multi_schedule(so, 8, 0, REFINE)
+        for d in range(1, 8):  # a shard's pieces: the same rule applied to the shard's slice
+            mine = [p for p in P if p["dev"] == d]
+            if not mine:
+                continue
+            a, b = mine[0]["lo"], mine[-1]["hi"]
+            want = sorted(set(int(x) for x in SH.ragged_bounds(so[a:b + 1] - so[a], 4)))
+            assert [p["lo"] - a for p in mine] + [b - a] == want
+
+
+def test_schedule_host_time_at_8_devices(lib):
+    """Round 5: the host-side work of a multi-GPU refinement call
+    before its first RCCL transfer -- the offsets' ends and cuts, the whole schedule (shards
+    and pieces by binary search, workspaces, transfers) -- for 1,048,576 ragged trajectories
+    over 8 devices, timed on the C call alone (tgms_multi_schedule with TGMS_SCHED_REFINE
+    runs exactly that work): median <= 0.1 ms.  The solve's schedule keeps its validation
+    pass (printed beside)."""
+    import ctypes
+    import time
+    from trajectory_generator_ros2_amd import _lib
+    from trajectory_generator_ros2_amd import synthetic as SY
+    so = SY.ragged_batch(1 << 20, 2, 16, seed=3)[0].astype(np.int32)
+    B, n = len(so) - 1, 8
+    bounds, ws = np.zeros(n + 1, np.int32), np.zeros(n, np.int64)
+    pieces, xfers = (_lib.Piece * 64)(), (_lib.Xfer * 1024)()
+    npc, nx = ctypes.c_int32(0), ctypes.c_int32(0)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+
+    def med(flags):
+        ts = []
+        for _ in range(31):
+            t0 = time.perf_counter()
+            st = lib.tgms_multi_schedule(n, B, ptr(so), 0, flags, ptr(bounds), ptr(ws), pieces, 64,
+                                         ctypes.byref(npc), xfers, 1024, ctypes.byref(nx))
+            ts.append(time.perf_counter() - t0)
+            assert st == 0
+        return sorted(ts)[15]
+    refine = med(REFINE | 4 | 8 | 16)
+    solve = med(SOLVE | 4 | 8)
+    print(f"tgms_multi_schedule n=8 B=1,048,576 ragged: refinement loop {refine * 1e3:.4f} ms "
+          f"({npc.value} pieces, {nx.value} transfers), solve (validation pass) {solve * 1e3:.3f} ms")
+    assert refine <= 1e-4

@@ -125,3 +125,36 @@ def test_shape_source_rejects(node_lib, override):
     p.pop("seg_times")
     p["v_goals"] = [1.0]
     assert not MinSnapNode(p).read_parameters()
+
+
+def test_config1_node_on_the_host_backend(node_lib, oracle):
+    """BASELINE config 1 ("ROS2 node up, no GPU"): with `minsnap_backend: host` the node
+    generates its goals on the CPU through the explicit host backend (tgms_create_host),
+    with the GPU path's conventions (Line.cpp:80-82 pinned end, frame_id "world",
+    power = true), matching the oracle at 1e-9.  Runs with or without a GPU present."""
+    from trajectory_generator_ros2_amd.node import MinSnapNode
+    n = MinSnapNode(base_params(minsnap_backend="host"))
+    assert n.read_parameters()
+    W = np.array(WAYPOINTS).reshape(-1, 3)
+    T = np.array([2.0, 2.0, 2.5])
+    C = n.coefficients()
+    R, st = oracle.solve(W, T)
+    assert st == 0
+    assert (np.abs(C - R).max(axis=(0, 2)) / np.abs(R).max(axis=(0, 2))).max() <= 1e-9
+    cnt = n.generate_traj()
+    G = n.goals()
+    ref = oracle.sample(R, T, W, None, 0.01, oracle.YAW_CONSTANT, 0.3)
+    assert cnt == G.shape[0] == ref.shape[0]
+    assert np.abs(G[:, :14] - ref[:, :14]).max() <= 1e-9 * max(1.0, np.abs(ref[:, :12]).max())
+    assert (G[:, 14] == 1.0).all() and n.frame_id(cnt - 1) == "world"
+    np.testing.assert_array_equal(G[-1, :3], W[-1])
+    # braking from the middle of the trajectory, as modeCB END does (replaces, pub_index 0)
+    k = n.generate_stop_traj(cnt // 2)
+    assert k > 0 and n.pub_index == 0
+    Gs = n.goals()
+    np.testing.assert_array_equal(Gs[-1, 3:12], np.zeros(9))
+
+
+def test_backend_parameter_is_checked(node_lib):
+    from trajectory_generator_ros2_amd.node import MinSnapNode
+    assert not MinSnapNode(base_params(minsnap_backend="cuda")).read_parameters()

@@ -76,3 +76,32 @@ def test_refinement_lowers_cost(oracle):
     assert (c10 <= c0 * (1 + 1e-12)).mean() > 0.95
     assert np.median(c10 / c0) < 0.95
     assert (Tn > 0).all()
+
+
+@pytest.mark.parametrize("M", [1, 3, 7, 12])
+def test_refine_grad_is_the_step_gradient(oracle, M):
+    """oracle.refine_grad (the per-segment dJ_i/dT_i and F at fixed times, used to pin one
+    GPU step at 1e-9) equals the gradient oracle_refine_times applies, and central finite
+    differences of the re-solved cost."""
+    rng = np.random.default_rng(40 + M)
+    _, W, T = S.uniform_batch(3, M, seed=41 + M)
+    kT = 0.3
+    for b in range(3):
+        ED = rng.normal(size=18) if b == 2 else None
+        dJ, F, st = oracle.refine_grad(W[b], T[b], ED, kT, oracle.REDUCED)
+        assert st == 0
+        eta = 1e-9
+        Tn, F0, _, st = oracle.refine_times(W[b], T[b], ED, kT, eta, 1, oracle.REDUCED)
+        assert st == 0
+        _, Fr, _, _ = oracle.refine_times(W[b], T[b], ED, kT, 0.0, 0, oracle.REDUCED)
+        assert F == Fr
+        g = -np.log(Tn / T[b]) * F / (eta * T[b]) - kT
+        assert np.abs(g - dJ).max() <= 1e-5 * np.abs(dJ).max()
+        i = M // 2
+        h = 1e-6 * T[b][i]
+        Tp, Tm = T[b].copy(), T[b].copy()
+        Tp[i] += h
+        Tm[i] -= h
+        fp = oracle.refine_times(W[b], Tp, ED, kT, 0.0, 0, oracle.REDUCED)[1]
+        fm = oracle.refine_times(W[b], Tm, ED, kT, 0.0, 0, oracle.REDUCED)[1]
+        assert abs((fp - fm) / (2 * h) - (dJ[i] + kT)) <= 1e-4 * (abs(dJ[i]) + kT)

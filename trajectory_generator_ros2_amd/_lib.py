@@ -14,14 +14,14 @@ from .build import LIB_TGMS
 OK, ERR_INVALID_ARG, ERR_SINGULAR, ERR_NONFINITE, ERR_NO_DEVICE, ERR_DEVICE, ERR_UNSUPPORTED = range(7)
 METHOD_REDUCED, METHOD_DENSE_KKT, METHOD_BAND_KKT = 0, 1, 2
 YAW_CONSTANT, YAW_VELOCITY = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_SEGMENTS = 16
 DENSE_MAX_SEGMENTS = 10
 GOAL_STRIDE = 14
 
 # Every symbol include/tgms.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [
-    "tgms_abi_version", "tgms_status_string", "tgms_create", "tgms_destroy", "tgms_last_error",
+    "tgms_abi_version", "tgms_status_string", "tgms_create", "tgms_create_host", "tgms_destroy", "tgms_last_error",
     "tgms_set_method", "tgms_solve_batch", "tgms_solve_uniform_device", "tgms_solve_batch_device",
     "tgms_sample_count", "tgms_sample_offsets", "tgms_sample_batch", "tgms_sample_batch_device",
     "tgms_refine_uniform_device", "tgms_refine_batch_device", "tgms_refine_loop_device", "tgms_refine_batch",
@@ -35,7 +35,7 @@ SCHED_REFINE, SCHED_END_DERIVS, SCHED_COEFFS, SCHED_STATUS, SCHED_COST, SCHED_SE
 class Piece(ctypes.Structure):
     """tgms_piece (include/tgms.h): one piece of one device's shard."""
     _fields_ = [("dev", ctypes.c_int32), ("piece", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
-                ("s0", ctypes.c_int64), ("s1", ctypes.c_int64), ("ws_off", ctypes.c_int64 * 9)]
+                ("s0", ctypes.c_int64), ("s1", ctypes.c_int64), ("ws_off", ctypes.c_int64 * 11)]
 
 
 class Xfer(ctypes.Structure):
@@ -76,6 +76,8 @@ def load(path: str = ""):
     L.tgms_status_string.restype = ctypes.c_char_p
     L.tgms_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
     L.tgms_create.restype = ctypes.c_int
+    L.tgms_create_host.argtypes = [ctypes.POINTER(vp)]
+    L.tgms_create_host.restype = ctypes.c_int
     L.tgms_destroy.argtypes = [vp]
     L.tgms_destroy.restype = None
     L.tgms_last_error.argtypes = [vp]

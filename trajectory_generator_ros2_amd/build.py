@@ -26,7 +26,7 @@ ARCH = os.environ.get("TGMS_ARCH", "gfx950")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 
 HIP_SOURCES = ["tgms_reduced.hip", "tgms_dense.hip", "tgms_band.hip", "tgms_sample.hip", "tgms_capi.hip"]
-CXX_SOURCES = ["tgms_plan.cpp"]  # host-only (no HIP): compiled by g++ into the same library
+CXX_SOURCES = ["tgms_plan.cpp", "tgms_host.cpp"]  # host-only (no HIP): compiled by g++ into the same library
 HOST_SOURCES = ["MinSnap.cpp", "factory.cpp", "tgms_node_capi.cpp"]
 
 

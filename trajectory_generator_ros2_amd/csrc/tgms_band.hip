@@ -145,7 +145,10 @@ __device__ __forceinline__ double recip(double x) {
 constexpr int QL = 4;                   // forward elimination: lanes per trajectory
 constexpr int QTW = W64 / QL;           // trajectories per wavefront
 constexpr int NJ = 6;                   // registers per window row and lane (slots 4 j + q)
-constexpr int QW = 4;                   // wavefronts per workgroup (share the pattern table)
+#ifndef TGMS_BAND_QW
+#define TGMS_BAND_QW 4
+#endif
+constexpr int QW = TGMS_BAND_QW;        // wavefronts per workgroup (share the pattern table)
 // Two wavefronts per SIMD (two workgroups per CU, TGMS_BAND_WAVES_PER_CU = 8): the window
 // (120 VGPRs), masks, multipliers, pivot and entering rows need ~290 registers, so within
 // 256 the compiler spills ~37 VGPRs (144 B of scratch per lane, a few per step);
@@ -186,6 +189,15 @@ __device__ __forceinline__ int dpp_i32(int v) {
 __device__ __forceinline__ int opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
+}
+
+// This lane's index in its wavefront, recomputed where it is used (volatile: never hoisted
+// or kept live across the sweep).  Used by the back substitution only: see the group loop
+// for the forward sweep's index.
+__device__ __forceinline__ int lane_now() {
+    int l = 0;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "+v"(l));
+    return l;
 }
 
 // Vc of segment i from the staged T_i (one lane of the quad writes it)
@@ -258,9 +270,19 @@ __device__ __forceinline__ double row_entry(int q, int pat_off, int rsrc, const 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Row positions: in registers (default, 10 VGPRs) or in the trajectory's LDS block.
+#ifndef TGMS_BAND_POS_LDS
+#define TGMS_BAND_POS_LDS 0
+#endif
+#if TGMS_BAND_POS_LDS
+typedef int* PosRef;
+#else
+typedef int (&PosRef)[WR];
+#endif
+
 template <int M, bool HAS_ED, int R>
-__device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)[WR][NJ], int (&pos)[WR],
-                                          bool& sing, __amdgpu_buffer_rsrc_t rs, const uint32_t vrow,
+__device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)[WR][NJ], PosRef P,
+                                          int& sing, __amdgpu_buffer_rsrc_t rs, const uint32_t vrow,
                                           const uint32_t vrow1, const uint32_t vrow5, const int* sd, double* X) {
     constexpr int N = 14 * M + 2;
     constexpr int JR = R / 4, O = R % 4;
@@ -273,33 +295,45 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
     double m = fabs(u[0][JR]);
 #pragma unroll
     for (int r = 1; r < WR; ++r) m = fmax(m, fabs(u[r][JR]));
-    int key = 0x7fffffff;
-#pragma unroll
-    for (int r = 0; r < WR; ++r) key = min(key, fabs(u[r][JR]) == m ? ((pos[r] << 4) | r) : 0x7fffffff);
-    sing = sing || (q == O && !(m > 0.0));
-    key = dpp_i32<BC>(key);  // lane O's pivot to the quad
-    const int ps = key & 15, cp = key >> 4;
-    double mr[WR];
-    double pv0 = 0.0, pv1 = 0.0;
+    // row positions from the trajectory's LDS block (registers are the scarce resource at
+    // two wavefronts per SIMD; the quad's lanes read the same words)
+#if TGMS_BAND_POS_LDS
+    int pos[WR];
+    {
+        const int4 pa = *reinterpret_cast<const int4*>(P), pb = *reinterpret_cast<const int4*>(P + 4);
+        const int2 pc = *reinterpret_cast<const int2*>(P + 8);
+        pos[0] = pa.x; pos[1] = pa.y; pos[2] = pa.z; pos[3] = pa.w;
+        pos[4] = pb.x; pos[5] = pb.y; pos[6] = pb.z; pos[7] = pb.w;
+        pos[8] = pc.x; pos[9] = pc.y;
+    }
+#else
+    int(&pos)[WR] = P;
+#endif
+    int key = 0x7fffffff, rk = 0;  // rk: the row at position k
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-        mr[r] = (ps == r) ? 1.0 : 0.0;
-        if (r & 1) pv1 = fma(mr[r], u[r][JR], pv1);
-        else pv0 = fma(mr[r], u[r][JR], pv0);
+        key = min(key, fabs(u[r][JR]) == m ? ((pos[r] << 4) | r) : 0x7fffffff);
+        rk = (pos[r] == k) ? r : rk;
     }
+    // folded in here (anchored): left to the compiler, the test sinks to the end of the
+    // unrolled steps and m or its flag is spilled across them
+    sing |= (q == O && !(m > 0.0)) ? 1 : 0;
+    asm volatile("" : "+v"(sing));
+    key = dpp_i32<BC>(key);  // lane O's pivot to the quad
+    const int ps = key & 15, cp = key >> 4;
+    // the pivot row by selection (exactly one row matches; no 0/1 multiplier registers)
+    double pv = u[0][JR];
+#pragma unroll
+    for (int r = 1; r < WR; ++r) pv = (ps == r) ? u[r][JR] : pv;
     // 1/pivot, formed in lane O, to the quad
-    const double inv = dpp_f64<BC>(recip(pv0 + pv1));
-    // the pivot row
+    const double inv = dpp_f64<BC>(recip(pv));
     double p[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        double a = mr[0] * u[0][j], b = mr[1] * u[1][j];
+        double a = u[0][j];
 #pragma unroll
-        for (int r = 2; r < WR; r += 2) {
-            a = fma(mr[r], u[r][j], a);
-            b = fma(mr[r + 1], u[r + 1][j], b);
-        }
-        p[j] = a + b;
+        for (int r = 1; r < WR; ++r) a = (ps == r) ? u[r][j] : a;
+        p[j] = a;
     }
     // U row k, scaled by 1/pivot, to the slab in slot order, laid out for 16-B accesses on
     // both sides: slots (s, s + 8), s < 8, as a 16-B pair at 16 s; slot s + 16 (s < 6) at
@@ -320,6 +354,9 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
 #endif
     }
     // the entering row k + 10
+#ifdef TGMS_BAND_SB1
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     double e[NJ];
     const int re = k + WR;
     if (re < N) {
@@ -341,29 +378,39 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) e[j] = 0.0;
     }
+#ifdef TGMS_BAND_SB2
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // rank-1 update; the pivot row cancels exactly and takes the entering row; column k
     // (lane O, register JR) restarts as column k + 19
-    const double keep = (q == O) ? 0.0 : 1.0;
-    p[JR] *= keep;
+    const bool restart = q == O;  // column k's register restarts (as column k + 19)
+    p[JR] = restart ? 0.0 : p[JR];
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-        // multiplier a_rk / a_pk (l_p = 1 exactly), formed in lane O (row r's column k is
-        // still unchanged there), to the quad
-        const double lr = dpp_f64<BC>(fma((ps == r) ? 0.0 : 1.0, u[r][JR] * inv, mr[r]));
+        // multiplier a_rk / a_pk, formed in lane O (row r's column k is still unchanged
+        // there), to the quad; the pivot row takes the entering row instead
+        const double lr = dpp_f64<BC>(u[r][JR] * inv);
+        const bool piv = ps == r;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const double base = (j == JR) ? u[r][j] * keep : u[r][j];
-            u[r][j] = fma(mr[r], e[j], fma(-lr, p[j], base));
+            const double base = (j == JR && restart) ? 0.0 : u[r][j];
+            const double nv = fma(-lr, p[j], base);
+            u[r][j] = piv ? e[j] : nv;
         }
     }
     // interchange: the row at position k takes the pivot's position; the pivot's slot
-    // holds row k + 10 now
+    // holds row k + 10 now (the second store wins when the pivot is the row at position k)
+#if TGMS_BAND_POS_LDS
+    P[rk] = cp;
+    P[ps] = re;
+#else
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
         int v = pos[r];
         v = (v == k) ? cp : v;
         pos[r] = (ps == r) ? re : v;
     }
+#endif
 }
 
 // Back substitution, eight lanes per trajectory, slot order.  Lane l holds slots l, l+8,
@@ -438,6 +485,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     constexpr int XL = x_len(M);
     __shared__ int s_desc[NPAT * WC];                  // pattern table of the interleaved KKT
     __shared__ double s_x[QW][QTW][XL];                // per-trajectory Vc | T | W | ED
+    __shared__ alignas(16) int s_pos[QW][QTW][12];     // per-trajectory row positions (10 used)
 
     for (int n = threadIdx.x; n < NPAT * WC; n += QW * W64) {
         const int pat = n / WC, d = n % WC - KL;
@@ -447,21 +495,29 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         s_desc[n] = (de == 0) ? pack_d(0, XZ) : pack_d(de >> 5, idx < VAL ? idx : idx - 1);
     }
     __syncthreads();
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / W64), lane = threadIdx.x % W64, g = lane / QL;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / W64);
     const int wave_id = blockIdx.x * QW + wv;  // wave-uniform (SGPR): the slab resource stays scalar
-    double* const X = s_x[wv][g];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         scratch + (size_t)wave_id * QTW * N * SW, (short)0, QTW * N * SW * 8, 0x00020000);
-    // this lane's places in a slab row: its pairs at 16 q (+ 64), its singles at 128 + 8 q (+ 32)
-    const uint32_t vrow = (uint32_t)(g * N * SW * 8 + 16 * (lane % QL));
-    const uint32_t vrow1 = (uint32_t)(g * N * SW * 8 + 128 + 8 * (lane % QL));
-    // register 5: the right-hand sides 1 and 2 (lanes 0, 1); lanes 2, 3 hold the unused
-    // slots 22, 23, which the slab does not keep (an out-of-range offset drops the store)
-    const uint32_t vrow5 = (lane % QL < 2) ? vrow1 + 32u : 0x7FFFFF00u;
     const int ngroups = (n_traj + QTW - 1) / QTW;
 
+    // The forward sweep's lane index from threadIdx.x (a value the compiler can range): taken
+    // from an inline-asm v_mbcnt at the top of each group instead (lane_now), the trajectories
+    // of quads 3, 7, 11 and 15 of a wave's second and later groups came out wrong with status
+    // OK (round 5, scripts/band_diag.py at M = 3 x 20,001: 160-251 of 20,001 wrong in every
+    // run; the same kernel with this line exact, A/B on one box, gpurun_out r05e); a wait for
+    // the previous group's memory traffic at the top of the group did not change it.
+    const int lane_top = threadIdx.x % W64;
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
+        const int lane = lane_top, g = lane / QL;
         const int q = opaque(lane % QL);
+        double* const X = s_x[wv][g];
+        // this lane's places in a slab row: its pairs at 16 q (+ 64), its singles at 128 + 8 q (+ 32)
+        const uint32_t vrow = (uint32_t)(g * N * SW * 8 + 16 * q);
+        const uint32_t vrow1 = (uint32_t)(g * N * SW * 8 + 128 + 8 * q);
+        // register 5: the right-hand sides 1 and 2 (lanes 0, 1); lanes 2, 3 hold the unused
+        // slots 22, 23, which the slab does not keep (an out-of-range offset drops the store)
+        const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
         const int bi = QTW * grp + g;
         const bool live = bi < n_traj;
         const int32_t b = ids ? ids[live ? bi : QTW * grp] : (live ? bi : QTW * grp);
@@ -498,7 +554,11 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
 
         // ---- the initial window: rows 0..9 over columns 0..18 (slot s = column s)
         double u[WR][NJ];
-        int pos[WR];
+#if TGMS_BAND_POS_LDS
+        int* const P = &s_pos[0][0][0] + (wv * QTW + g) * 12;
+#else
+        int P[WR];
+#endif
 #define IROW(RR)                                                                      \
     {                                                                                 \
         int pat_off, rsrc, seg;                                                       \
@@ -509,21 +569,22 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         u[RR][3] = row_entry<3, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
         u[RR][4] = row_entry<4, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
         u[RR][5] = row_entry<5, 0, 9 - RR>(q, pat_off, rsrc, s_desc, X);              \
-        pos[RR] = RR;                                                                 \
+        P[RR] = pos0 + RR;                                                            \
     }
+        const int pos0 = opaque(0);  // (a hoisted constant pair would be spilled over the sweep)
         IROW(0) IROW(1) IROW(2) IROW(3) IROW(4) IROW(5) IROW(6) IROW(7) IROW(8) IROW(9)
 #undef IROW
-        bool sing = false;
+        int sing = 0;
 
         // ---- forward elimination (a3)
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, pos, sing, rs, vrow, vrow1, vrow5, s_desc, X);
+    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, P, sing, rs, vrow, vrow1, vrow5, s_desc, X);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
         }
-        const unsigned long long singm = __ballot(sing);
+        const unsigned long long singm = __ballot(sing != 0);
 
         // ---- back substitution (round 3), 8-lane groups, eight trajectories per pass.  The U rows
         // this wave stored are read back by other lanes of the wave: wait for the stores to
@@ -535,10 +596,10 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         constexpr int kN = N - 1;
-        const int lb = opaque(lane % BL);
+        const int lane_b = lane_now(), lb = lane_b % BL;
 #pragma unroll 1
         for (int pass = 0; pass < QTW / BT; ++pass) {
-            const int slot = pass * BT + lane / BL;  // trajectory slot of this 8-lane group
+            const int slot = pass * BT + lane_b / BL;  // trajectory slot of this 8-lane group
             const int bq = QTW * grp + slot;
             const bool liveq = bq < n_traj;
             const int32_t bb = ids ? ids[liveq ? bq : QTW * grp] : (liveq ? bq : QTW * grp);
@@ -568,7 +629,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
 #undef BSTEP
             }
             const unsigned long long nf = __ballot(!(fin == 0.0));
-            const bool nonfinite = ((nf >> (BL * (lane / BL))) & 0xffull) != 0;
+            const bool nonfinite = ((nf >> (BL * (lane_b / BL))) & 0xffull) != 0;
             if (liveq && lb == 0 && status) {
                 int32_t st = TGMS_OK;
                 if (!valid) st = TGMS_ERR_INVALID_ARG;

@@ -79,19 +79,36 @@ hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, cons
                                const double* W, const double* T, const double* ED, double kT, double eta,
                                double* Tout, double* cost, double* C, int32_t* status, hipStream_t stream);
 
-// The whole refinement loop of a ragged batch per occupancy class in one launch: iters
-// steps, the cost at the final times (cost nullable), the final solve into C (nullable);
-// T holds the initial times and receives the final ones (in place).
-hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* seg_offsets, const double* W,
-                                    double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
-                                    double* C, int32_t* status, hipStream_t stream);
-
 // The M-grouping permutation of a ragged batch computed on the device (stable counting
 // sort of the ids by so[b+1] - so[b]; M validated on the host): starts[m] (m = 1..16) is
 // where group m begins, hist a workspace of perm_hist_bytes(B).
 size_t perm_hist_bytes(int32_t B);
 hipError_t launch_group_perm(int32_t B, const int32_t* seg_offsets, const int32_t* starts, int32_t* hist,
                              int32_t* perm, hipStream_t stream);
+
+// The launch plan of a ragged refinement loop computed entirely on the device (round 5):
+// the per-M totals summed from k_perm_hist's block counts, the starts of the M groups in
+// the permutation and both occupancy classes' group tables.  The host plans nothing per
+// trajectory, and a captured graph stays valid for any offsets of the same B and S: each
+// replay regroups.  `so` may be a slice of a larger batch's offsets (so[0] != 0: the
+// kernels subtract so_base = so[0]); offsets whose M leave 1..16 or whose span is not S
+// mark the plan bad and nothing runs: statuses TGMS_ERR_INVALID_ARG, the S segments'
+// coefficients (C, nullable) and the n costs (cost, nullable) exact zeros, times kept.
+// This is the only per-trajectory check of tgms_refine_loop_multi_device's offsets.
+struct DevPlan {
+    GroupTable tab[2];
+    int32_t starts[17];  // starts[m]: first index of group m in the permutation (m = 1..16)
+    int32_t so_base;     // so[0]
+    int32_t bad;
+};
+// Grid of one class's loop launch: every wavefront a group table can hold, whatever the
+// offsets (the blocks beyond the class's last group return at once).
+inline unsigned dev_loop_grid(int32_t n) { return (unsigned)((n + RAGGED_TPW - 1) / RAGGED_TPW + 16); }
+hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int has_ed, int32_t* hist, int32_t* perm,
+                                 DevPlan* plan, int32_t* status, double* C, double* cost, hipStream_t stream);
+hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+                                  double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
+                                  double* C, int32_t* status, hipStream_t stream);
 
 // Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,

@@ -50,6 +50,28 @@ void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* b
         bounds[parts] = B;
         return;
     }
+    if (method != TGMS_METHOD_DENSE_KKT && uniform_m <= 0) {
+        // the running cost 2 (b + 1) + so[b + 1] - so[0] is an integer below 2^53, so the fp64
+        // prefix sum below would hold it exactly: the same cuts by binary search
+        const int32_t so0 = so[0];
+        auto c_at = [&](int64_t b) { return (double)(2 * (b + 1) + ((int64_t)so[b + 1] - so0)); };
+        const double total = c_at(B - 1);
+        int64_t prev = 0;
+        for (int k = 1; k < parts; ++k) {
+            const double target = (total * (double)k) / (double)parts;
+            int64_t lo = 0, hi = B;  // lower_bound: first b with c(b) >= target
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if (c_at(mid) < target) lo = mid + 1;
+                else hi = mid;
+            }
+            int64_t cut = std::max(lo + 1, prev);
+            prev = cut;
+            bounds[k] = (int32_t)std::min<int64_t>(cut, B);
+        }
+        bounds[parts] = B;
+        return;
+    }
     std::vector<double> c(B);
     double acc = 0.0;
     for (int32_t b = 0; b < B; ++b) {
@@ -67,6 +89,16 @@ void plan_shards(int32_t B, const int32_t* so, int parts, int method, int32_t* b
     bounds[parts] = B;
 }
 
+bool cuts_valid(const MultiPlan& P, const int32_t* so) {
+    auto ok = [](int64_t n, int64_t span) { return n >= 0 && span >= n && span <= (int64_t)TGMS_MAX_SEGMENTS * n; };
+    for (int d = 0; d < P.n; ++d) {
+        if (!ok(P.bounds[d + 1] - P.bounds[d], (int64_t)so[P.bounds[d + 1]] - so[P.bounds[d]])) return false;
+        for (const PiecePlan& p : P.pieces[d])
+            if (!ok(p.n(), p.S())) return false;
+    }
+    return true;
+}
+
 void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, const MultiFlags& f, MultiPlan* out) {
     MultiPlan& P = *out;
     P.n = n;
@@ -82,13 +114,14 @@ void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, 
         const int32_t lo = P.bounds[d], hi = P.bounds[d + 1];
         if (hi <= lo) continue;
         int32_t pb[MULTI_PIECES + 1];
-        if (uniform_m > 0) {
+        if (uniform_m > 0)
             plan_shards(hi - lo, nullptr, MULTI_PIECES, method, pb, uniform_m);
-        } else {
-            std::vector<int32_t> so_l(hi - lo + 1);
-            for (int32_t b = lo; b <= hi; ++b) so_l[b - lo] = so[b] - so[lo];
-            plan_shards(hi - lo, so_l.data(), MULTI_PIECES, method, pb);
-        }
+        else
+            plan_shards(hi - lo, so + lo, MULTI_PIECES, method, pb);  // the shard's slice, no copy
+        // ragged solve: host-planned pieces (plan block uploaded); ragged refinement loop:
+        // planned on the device (offsets slice scattered with the inputs)
+        const bool host_plan = uniform_m <= 0 && !f.refine;
+        const bool dev_plan = uniform_m <= 0 && f.refine;
         std::vector<PiecePlan>& ps = P.pieces[d];
         size_t plan_bytes = 0;
         for (int k = 0; k < MULTI_PIECES; ++k) {
@@ -98,14 +131,26 @@ void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, 
             p.hi = lo + pb[k + 1];
             p.s0 = so ? so[p.lo] : (int64_t)p.lo * uniform_m;
             p.s1 = so ? so[p.hi] : (int64_t)p.hi * uniform_m;
-            p.oSo = plan_bytes;
-            plan_bytes = align256(plan_bytes + sizeof(int32_t) * (p.n() + 1));
-            p.oPerm = plan_bytes;
-            plan_bytes = align256(plan_bytes + sizeof(int32_t) * p.n());
+            if (host_plan) {
+                p.oSo = plan_bytes;
+                plan_bytes = align256(plan_bytes + sizeof(int32_t) * (p.n() + 1));
+                p.oPerm = plan_bytes;
+                plan_bytes = align256(plan_bytes + sizeof(int32_t) * p.n());
+            }
             ps.push_back(p);
         }
         size_t off = plan_bytes;  // the plan block (mirrored in the pinned staging) comes first
         for (PiecePlan& p : ps) {
+            if (dev_plan) {
+                p.oSo = off; off = align256(off + sizeof(int32_t) * (p.n() + 1));
+                p.oPerm = off; off = align256(off + sizeof(int32_t) * p.n());
+                p.oHist = off; off = align256(off + dev_hist_bytes(p.n()));
+                p.oPlan = off; off = align256(off + DEV_PLAN_BYTES);
+            } else if (!host_plan) {
+                p.oSo = p.oPerm = p.oHist = p.oPlan = off;  // (empty regions)
+            } else {
+                p.oHist = p.oPlan = off;
+            }
             p.oW = off; off = align256(off + 8 * (size_t)(p.S() + p.n()) * 3);
             p.oT = off; off = align256(off + 8 * (size_t)p.S());
             p.oT2 = off; off = align256(off + (f.refine ? 8 * (size_t)p.S() : 0));
@@ -127,6 +172,8 @@ void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, 
             P.xfers.push_back({d, k, 0, XA_W, (p.s0 + p.lo) * 3, (int64_t)p.oW, (p.S() + p.n()) * 3, 8, k});
             P.xfers.push_back({d, k, 0, XA_T, p.s0, (int64_t)p.oT, p.S(), 8, k});
             if (f.has_ed) P.xfers.push_back({d, k, 0, XA_ED, (int64_t)p.lo * 18, (int64_t)p.oED, (int64_t)p.n() * 18, 8, k});
+            if (f.refine && uniform_m <= 0)  // the raw offsets slice for the device-side plan
+                P.xfers.push_back({d, k, 0, XA_SO, (int64_t)p.lo, (int64_t)p.oSo, (int64_t)p.n() + 1, 4, k});
         }
     for (int k = 0; k < MULTI_PIECES; ++k)
         for (int d = 0; d < n; ++d) {

@@ -895,6 +895,44 @@ __device__ __forceinline__ void pin33(double (&m)[3][3]) {
         for (int j = 0; j < 3; ++j) pin(m[i][j]);
 }
 
+// Whole-line output of the joint solve (uniform batches, even M; PairLineOut below): the
+// three axes of a segment are emitted together, as whole 128-B lines.
+struct PairLineOut;
+template <class T>
+struct is_pair_lines : std::false_type {};
+template <>
+struct is_pair_lines<PairLineOut> : std::true_type {};
+template <int M>
+__device__ __forceinline__ void pair_emit_lines(const PairLineOut& o, int j, bool right, const double (&c)[3][8]);
+template <int M>
+__device__ __forceinline__ void pair_flush_lines(const PairLineOut& o);
+
+// Monomial coefficients of one axis of a segment from its Hermite data (emit_axis_v's
+// arithmetic), zeroed for a failed factorisation.
+__device__ __forceinline__ void axis_coeffs(double ws, double we, double r, bool right, const double (&xs)[3],
+                                            const double (&xe)[3], bool zero, double (&c)[8]) {
+    const double w0 = right ? we : ws, w1 = right ? ws : we;
+    const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
+    const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
+    const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
+    const double D = (w1 - w0) * r3;
+    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
+    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
+    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
+    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
+    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+    c[0] = w0;
+    c[1] = v0;
+    c[2] = 0.5 * a0;
+    c[3] = j0 * (1.0 / 6.0);
+    c[4] = P4 * r;
+    c[5] = P5 * r2;
+    c[6] = P6 * r3;
+    c[7] = P7 * r4;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = zero ? 0.0 : c[k];
+}
+
 // The same solve with the three axes side by side in every knot step (knot-major
 // instead of axis-major), for the kernels that run at one wave per SIMD anyway
 // (M > TGMS_TWO_WAVE_MAX_M): the per-knot couplings and powers are formed once
@@ -1085,7 +1123,16 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
 #pragma unroll
                 for (int d = 0; d < 3; ++d) Y[s][a][d] = at_end ? xm[a][d] : Y[s][a][d];
         }
-        if (s + 1 < NE) {
+        if constexpr (is_pair_lines<Out>::value) {
+            if (s + 1 < NE) {
+                double c[3][8];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+                    axis_coeffs(L.w(s + 1, a), L.w(s + 2, a), L.r(s + 1), right, Y[s][a], Y[s + 1][a], !spd_pair,
+                                c[a]);
+                pair_emit_lines<M>(O, NE - 1 - (s + 1), right, c);
+            }
+        } else if (s + 1 < NE) {
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #if TGMS_JOINT_PREFETCH
@@ -1105,13 +1152,21 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
 #endif
     }
     SCHED_FENCE();
+    if constexpr (is_pair_lines<Out>::value) {
+        double c[3][8];
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+        for (int a = 0; a < 3; ++a) axis_coeffs(L.w(0, a), L.w(1, a), L.r(0), right, u0[a], Y[0][a], !spd_pair, c[a]);
+        pair_emit_lines<M>(O, NE - 1, right, c);
+        pair_flush_lines<M>(O);
+    } else {
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
 #if TGMS_JOINT_PREFETCH
-        emit_axis_v<M, Out>(O, w_lo[a], w_hi[a], r_n, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+            emit_axis_v<M, Out>(O, w_lo[a], w_hi[a], r_n, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
 #else
-        emit_axis<M, Out>(O, L, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
+            emit_axis<M, Out>(O, L, right, 0, a, u0[a], Y[0][a], 0 < nR, !spd_pair);
 #endif
+    }
     const double fin_pair = fin + pair_swap(fin);
     if (!valid) return TGMS_ERR_INVALID_ARG;
     if (!spd_pair) return TGMS_ERR_SINGULAR;
@@ -1567,7 +1622,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
                                                   const double* __restrict__ W, double* __restrict__ T,
                                                   const double* __restrict__ ED, double kT, double eta,
                                                   int32_t iters, double* __restrict__ cost, double* __restrict__ C,
-                                                  int32_t* __restrict__ status) {
+                                                  int32_t* __restrict__ status, int32_t so_base) {
     using CH = Chain<M>;
     constexpr int NE = CH::NE;
     constexpr int NW = (M + 1) * 3;
@@ -1586,7 +1641,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
     int64_t s0 = 0;
     if (live) {
         b = perm[i0 + slot];
-        s0 = seg_offsets[b];
+        s0 = (int64_t)seg_offsets[b] - so_base;  // (a slice of a larger batch's offsets: rebased)
         if (!right) sm.in.base[slot] = s0 * 24;
         const double* gW = W + (s0 + b) * 3;
         for (int q = right; q < NW; q += 2) stage_row_w(sm.in, slot, q, gW[q]);
@@ -1764,25 +1819,32 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_multi(GroupTable
     }
 }
 
+// The refinement loop with the device-computed plan (k_group_plan): the class's group
+// table is read from device memory (scalar loads), the grid covers every wavefront a
+// table can hold (dev_loop_grid) and the blocks past the class's last group return.
 template <int MLO, int MHI, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_multi(GroupTable tab,
-                                                                            const int32_t* __restrict__ seg_offsets,
-                                                                            const double* __restrict__ W,
-                                                                            double* __restrict__ T,
-                                                                            const double* __restrict__ ED, double kT,
-                                                                            double eta, int32_t iters,
-                                                                            double* __restrict__ cost,
-                                                                            double* __restrict__ C,
-                                                                            int32_t* __restrict__ status) {
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_dev(const DevPlan* __restrict__ plan, int cls,
+                                                                          const int32_t* __restrict__ seg_offsets,
+                                                                          const double* __restrict__ W,
+                                                                          double* __restrict__ T,
+                                                                          const double* __restrict__ ED, double kT,
+                                                                          double eta, int32_t iters,
+                                                                          double* __restrict__ cost,
+                                                                          double* __restrict__ C,
+                                                                          int32_t* __restrict__ status) {
     __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
+    const GroupTable& tab = plan->tab[cls];
+    const int ng = tab.ngroups;
+    if (ng <= 0 || (int64_t)blockIdx.x >= tab.blk_end[ng - 1]) return;
     int64_t blk;
     const int g = group_of(tab, blockIdx.x, blk);
+    const int32_t so_base = plan->so_base;
     switch (tab.m[g]) {
 #define TGMS_MULTI_CASE(mm)                                                                                    \
     case mm:                                                                                                  \
         if constexpr (mm >= MLO && mm <= MHI)                                                                 \
             refine_loop_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g],     \
-                                          seg_offsets, W, T, ED, kT, eta, iters, cost, C, status);           \
+                                          seg_offsets, W, T, ED, kT, eta, iters, cost, C, status, so_base);  \
         break;
         TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
         TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
@@ -1830,9 +1892,10 @@ struct PermStarts {
     int32_t s[PERM_BINS];  // first index of group M in the permutation
 };
 
-__global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const int32_t* __restrict__ so,
-                                                             const int32_t* __restrict__ hist, PermStarts st,
-                                                             int32_t* __restrict__ perm) {
+template <class Starts>
+__device__ __forceinline__ void perm_scatter_body(int32_t B, const int32_t* __restrict__ so,
+                                                  const int32_t* __restrict__ hist, Starts&& start_of,
+                                                  int32_t* __restrict__ perm) {
     __shared__ int32_t wc[PERM_BLOCK / W64][PERM_BINS];
     __shared__ int32_t base[PERM_BINS];
     const int t = threadIdx.x, w = t / W64, l = t % W64;
@@ -1851,7 +1914,7 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const in
         for (unsigned v = l; v < blockIdx.x; v += W64) s += hist[(int64_t)v * PERM_BINS + g];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if (l == 0) base[g] = st.s[g] + s;
+        if (l == 0) base[g] = start_of(g) + s;
     }
     __syncthreads();
     if (m >= 1 && m < PERM_BINS) {  // (a device copy of the offsets that disagrees with the
@@ -1860,6 +1923,92 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const in
         r += __popcll(mine & ((1ull << l) - 1ull));
         if (r >= 0 && r < B) perm[r] = (int32_t)b;
     }
+}
+
+__global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const int32_t* __restrict__ so,
+                                                             const int32_t* __restrict__ hist, PermStarts st,
+                                                             int32_t* __restrict__ perm) {
+    perm_scatter_body(B, so, hist, [&](int g) { return st.s[g]; }, perm);
+}
+
+__global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter_dev(int32_t B, const int32_t* __restrict__ so,
+                                                                 const int32_t* __restrict__ hist,
+                                                                 const DevPlan* __restrict__ plan,
+                                                                 int32_t* __restrict__ perm) {
+    if (plan->bad) return;
+    perm_scatter_body(B, so, hist, [&](int g) { return plan->starts[g]; }, perm);
+}
+
+// The device-side plan (DevPlan, tgms_internal.h) from k_perm_hist's block counts: one
+// workgroup sums them per M (16 bins x 64 strided partial sums), checks the offsets against
+// the host's B and S, and thread 0 lays out the starts and both classes' group tables in
+// the order the host planner used (M descending within a class).  A bad plan runs nothing
+// and marks every trajectory TGMS_ERR_INVALID_ARG, its outputs exact zeros (rare path: one
+// workgroup clears the S x 24 coefficients).
+constexpr int PLAN_THREADS = 1024;
+__global__ __launch_bounds__(PLAN_THREADS) void k_group_plan(int32_t n, int64_t S, const int32_t* __restrict__ so,
+                                                            int has_ed, const int32_t* __restrict__ hist,
+                                                            int32_t* __restrict__ perm, DevPlan* __restrict__ plan,
+                                                            int32_t* __restrict__ status, double* __restrict__ C,
+                                                            double* __restrict__ cost) {
+    constexpr int NPART = PLAN_THREADS / 16;
+    __shared__ int32_t part[NPART][PERM_BINS];
+    __shared__ int32_t cnt[PERM_BINS];
+    __shared__ int32_t bad_s;
+    const int t = threadIdx.x;
+    const int nblk = (n + PERM_BLOCK - 1) / PERM_BLOCK;
+    {
+        const int bin = (t & 15) + 1, j0 = t >> 4;
+        int32_t s = 0;
+        for (int v = j0; v < nblk; v += NPART) s += hist[(int64_t)v * PERM_BINS + bin];
+        part[j0][bin] = s;
+    }
+    __syncthreads();
+    if (t < 16) {
+        int32_t c = 0;
+        for (int j = 0; j < NPART; ++j) c += part[j][t + 1];
+        cnt[t + 1] = c;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int64_t tot = 0;
+        for (int m = 1; m < PERM_BINS; ++m) tot += cnt[m];
+        const int32_t so0 = so[0];
+        const bool bad = tot != n || (int64_t)so[n] - so0 != S;
+        plan->so_base = so0;
+        plan->bad = bad ? 1 : 0;
+        bad_s = bad ? 1 : 0;
+        const int max2 = has_ed ? TGMS_TWO_WAVE_MAX_M_ED : TGMS_TWO_WAVE_MAX_M;
+        int32_t st = 0;
+        plan->starts[0] = 0;
+        for (int m = 1; m < PERM_BINS; ++m) {
+            plan->starts[m] = st;
+            st += bad ? 0 : cnt[m];
+        }
+        int ng[2] = {0, 0};
+        int32_t be[2] = {0, 0};
+        for (int m = PERM_BINS - 1; m >= 1; --m) {
+            if (bad || !cnt[m]) continue;
+            const int c = m > max2 ? 1 : 0;
+            GroupTable& tb = plan->tab[c];
+            const int g = ng[c]++;
+            be[c] += (cnt[m] + RAGGED_TPW - 1) / RAGGED_TPW;
+            tb.m[g] = m;
+            tb.n[g] = cnt[m];
+            tb.perm[g] = perm + plan->starts[m];
+            tb.blk_end[g] = be[c];
+        }
+        plan->tab[0].ngroups = ng[0];
+        plan->tab[1].ngroups = ng[1];
+    }
+    __syncthreads();
+    if (!bad_s) return;
+    for (int64_t b = t; b < n; b += PLAN_THREADS) {
+        if (status) status[b] = TGMS_ERR_INVALID_ARG;
+        if (cost) cost[b] = 0.0;
+    }
+    if (C)
+        for (int64_t i = t; i < S * 24; i += PLAN_THREADS) C[i] = 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2014,6 +2163,215 @@ __device__ __forceinline__ void put_segment_lines_store(const LineOut& o, int e,
                                                         const StagedLine& L1) {
     store_line(o, L0, seg_line_off(e, 0));
     if (seg_lines(e) == 2) store_line(o, L1, seg_line_off(e, 1));
+}
+
+// ---------------------------------------------------------------------------
+// Whole-line output of the joint lane-pair solve (uniform batches, even M >= 12): the even
+// lane emits its segments nL, nL-1, .., 0 (nL = M/2 - 1), the odd lane nL+1, .., M-1, one
+// segment per step each, all three axes at once.  A segment pair (2k, 2k+1) is three 128-B
+// lines of [traj][seg][axis][8]: (2k: x y), (2k: z | 2k+1: x), (2k+1: y z).  The even lane
+// meets a pair at its odd segment first: it stages (y z) and carries x; the odd lane meets it
+// at its even segment: it stages (x y) and carries z; the next step completes the other two
+// lines.  At every step both lanes of a pair stage the same number of lines (their segments
+// have opposite parity), except at step 0 when nL is even: then the middle pair (nL, nL+1)
+// is split between the lanes and the even lane completes (nL: z | nL+1: x) with the odd
+// lane's x row (DPP swap).  Lines go through the lane kernel's transposed LDS stage: a lane
+// stores rows (lane >> 3) + 8 q, all of one parity, so its line offsets are the even or the
+// odd lane's, and eight buffer resources of four trajectories each drop a tail wave's
+// missing trajectories (range check).  Half-line stores a pass apart run at ~3.4 TB/s past
+// the Infinity Cache, whole lines at ~5.5 (scripts/storebench.hip).
+struct PairLineOut {
+    double* stage[2];              // LDS [W64][LROW]
+    __amdgpu_buffer_rsrc_t rs[8];  // store q: trajectories 4q .. 4q+3 of the wave's block
+    uint32_t voff;                 // (lane >> 4) * TRAJ_B + (lane & 7) * 16
+    bool odd_rows;                 // the rows this lane stores were staged by odd (right) lanes
+    bool nt;                       // streaming stores
+    int lane;
+    mutable double carry[8];
+};
+
+template <int M>
+__device__ __forceinline__ PairLineOut make_pair_line_out(double* s0, double* s1, double* C, int64_t b0, int nb,
+                                                          int lane, bool nt) {
+    constexpr int TRAJ_B = M * 24 * 8;
+    PairLineOut o;
+    o.stage[0] = s0;
+    o.stage[1] = s1;
+    o.lane = lane;
+    o.nt = nt;
+    double* base = C + b0 * (M * 24);
+    const int block = nb * TRAJ_B;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int lim = block - q * 4 * TRAJ_B;
+        o.rs[q] = __builtin_amdgcn_make_buffer_rsrc(base + (int64_t)q * 4 * M * 24, (short)0, lim > 0 ? lim : 0,
+                                                    0x00020000);
+    }
+    o.voff = (uint32_t)((lane >> 4) * TRAJ_B + (lane & 7) * 16);
+    o.odd_rows = (lane >> 3) & 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.carry[k] = 0.0;
+    return o;
+}
+
+// Step j's lines: count per lane (1 or 2) and byte offsets in the trajectory's block for
+// the even and the odd lane (-1: none).  Constant-folded: j is a compile-time index.
+template <int M>
+__device__ __forceinline__ void pair_line_step(int j, int& nbuf, int (&offE)[2], int (&offO)[2]) {
+    constexpr int nL = M / 2 - 1;
+    const int eE = nL - j, eO = nL + 1 + j;
+    if (j == 0 && nL % 2 == 0) {  // the middle pair split between the lanes
+        nbuf = 2;
+        offE[0] = eE * 192, offE[1] = eE * 192 + 128;
+        offO[0] = eO * 192 + 64, offO[1] = -1;
+    } else if (eE & 1) {
+        nbuf = 1;
+        offE[0] = eE * 192 + 64, offE[1] = -1;
+        offO[0] = eO * 192, offO[1] = -1;
+    } else {
+        nbuf = 2;
+        offE[0] = eE * 192, offE[1] = eE * 192 + 128;
+        offO[0] = eO * 192 - 64, offO[1] = eO * 192 + 64;
+    }
+}
+
+__device__ __forceinline__ void pair_store_line(const PairLineOut& o, const StagedLine& L, int offE, int offO) {
+    const int off = o.odd_rows ? offO : offE;
+    const uint32_t v = off >= 0 ? o.voff + (uint32_t)off : 0x80000000u;  // none: out of range, dropped
+    if (o.nt) {  // wave-uniform
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, L.v[q]), o.rs[q], v, 0,
+                                                   TGMS_STORE_CPOL_NT);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, L.v[q]), o.rs[q], v, 0, TGMS_STORE_CPOL);
+    }
+}
+
+__device__ __forceinline__ void pair_read_line(const PairLineOut& o, int buf, StagedLine& L) {
+    const double* src = o.stage[buf] + (o.lane >> 3) * LROW + (o.lane & 7) * 2;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) L.v[q] = *reinterpret_cast<const double2*>(src + q * 8 * LROW);
+}
+
+__device__ __forceinline__ void pair_stage_line(const PairLineOut& o, int buf, const double (&lo)[8],
+                                                const double (&hi)[8]) {
+    double2* d = reinterpret_cast<double2*>(o.stage[buf] + o.lane * LROW);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = make_double2(lo[2 * k], lo[2 * k + 1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[4 + k] = make_double2(hi[2 * k], hi[2 * k + 1]);
+}
+
+// Emission step j (c: this lane's segment, three axes): store the lines step j - 1 left
+// staged (software-pipelined: the LDS writes of a step land while the next one computes),
+// then stage this step's.
+template <int M>
+__device__ __forceinline__ void pair_emit_lines(const PairLineOut& o, int j, bool right, const double (&c)[3][8]) {
+    static_assert(M % 2 == 0, "whole lines need even M");
+    constexpr int nL = M / 2 - 1;
+    StagedLine P0, P1;
+    int pn = 0, pE[2] = {-1, -1}, pO[2] = {-1, -1};
+    if (j > 0) {
+        pair_line_step<M>(j - 1, pn, pE, pO);
+        wave_lds_sync();  // the previous step's stage writes have landed
+        pair_read_line(o, 0, P0);
+        if (pn == 2) pair_read_line(o, 1, P1);
+    }
+    const int eE = nL - j;
+    double lo[8], hi[8];
+    if (j == 0 && nL % 2 == 0) {
+        // even lane: (nL: x y) and (nL: z | nL+1: x), the odd lane's x row by DPP; odd lane:
+        // (nL+1: y z)
+        double xo[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xo[k] = pair_swap(c[0][k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo[k] = right ? c[1][k] : c[0][k];
+            hi[k] = right ? c[2][k] : c[1][k];
+        }
+        pair_stage_line(o, 0, lo, hi);
+        pair_stage_line(o, 1, c[2], xo);  // (the odd lane's copy is never stored)
+    } else if (eE & 1) {
+        // even lane at an odd segment: (y z), carry x; odd lane at an even one: (x y), carry z
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo[k] = right ? c[0][k] : c[1][k];
+            hi[k] = right ? c[1][k] : c[2][k];
+            o.carry[k] = right ? c[2][k] : c[0][k];
+        }
+        pair_stage_line(o, 0, lo, hi);
+    } else {
+        // even lane at an even segment: (x y), (z | carry); odd lane at an odd one: (carry | x), (y z)
+        double lo1[8], hi1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            lo[k] = right ? o.carry[k] : c[0][k];
+            hi[k] = right ? c[0][k] : c[1][k];
+            lo1[k] = right ? c[1][k] : c[2][k];
+            hi1[k] = right ? c[2][k] : o.carry[k];
+        }
+        pair_stage_line(o, 0, lo, hi);
+        pair_stage_line(o, 1, lo1, hi1);
+    }
+    if (j > 0) {
+        pair_store_line(o, P0, pE[0], pO[0]);
+        if (pn == 2) pair_store_line(o, P1, pE[1], pO[1]);
+    }
+}
+
+// After the last step (j = M/2 - 1): store what it staged.
+template <int M>
+__device__ __forceinline__ void pair_flush_lines(const PairLineOut& o) {
+    int pn = 0, pE[2], pO[2];
+    pair_line_step<M>(M / 2 - 1, pn, pE, pO);
+    StagedLine P0, P1;
+    wave_lds_sync();
+    pair_read_line(o, 0, P0);
+    if (pn == 2) pair_read_line(o, 1, P1);
+    pair_store_line(o, P0, pE[0], pO[0]);
+    if (pn == 2) pair_store_line(o, P1, pE[1], pO[1]);
+}
+
+template <int M>
+struct alignas(16) RawLineStage {
+    alignas(16) double O[2][W64 * LROW];  // two line buffers (the lane kernel's stage layout)
+    RawIn<M> in;
+};
+
+// Uniform batches with even M >= TGMS_PAIR_LINES_MIN_M: the joint lane-pair solve (one
+// wave per SIMD) with whole-line output; otherwise k_reduced_uniform.
+template <int M, bool HAS_ED>
+__global__ __launch_bounds__(64, 1) void k_reduced_uniform_lines(int32_t B, const double* __restrict__ W,
+                                                                 const double* __restrict__ T,
+                                                                 const double* __restrict__ ED,
+                                                                 double* __restrict__ C,
+                                                                 int32_t* __restrict__ status, int nt) {
+    __shared__ RawLineStage<M> sm;
+    const int lane = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * TPW;
+    const int nb = (int)((B - b0) < TPW ? (B - b0) : TPW);
+    RawLoader<M> ld;
+    ld.ed = HAS_ED ? ED : nullptr;
+    ld.issue(W, T, B, b0, nb, lane);
+    ld.stage_T(sm.in, W, T, b0, nb, lane);
+    const int slot = lane >> 1;
+    const bool right = lane & 1;
+    const bool live = slot < nb;
+    const int64_t b = b0 + slot;
+    auto stage_w = [&]() {
+        const bool any_bad = ld.stage_W(sm.in, W, T, b0, nb, lane);
+        return !any_bad || sm.in.bad[slot] == 0;
+    };
+    const LaneView L = make_view_raw<M>(sm.in, slot, right);
+    const PairLineOut O = make_pair_line_out<M>(sm.O[0], sm.O[1], C, b0, nb, lane, nt != 0);
+    const int32_t st =
+        pair_solve_joint<M, HAS_ED, PairLineOut>(L, right, stage_w, (HAS_ED && live) ? ED + b * 18 : ED, O);
+    if (live && st == TGMS_ERR_NONFINITE) zero_traj(C + b * (M * 24), M * 24, right, 2);
+    if (live && !right && status) status[b] = st;
 }
 
 // Monomial coefficients of segment e, all three axes, from the Hermite data at its
@@ -2369,11 +2727,20 @@ __global__ __launch_bounds__(64, 1) void k_lane_uniform(int32_t B, const double*
 // faster (60 vs 77 us, 69 vs 109 us; profiles/r04_lane_vs_pair_M12_16.jsonl), so M >= 14
 // take the lane-pair kernel.
 #ifndef TGMS_LANE_MAX_M
-#define TGMS_LANE_MAX_M 12
+#define TGMS_LANE_MAX_M 10
 #endif
 template <int M>
 constexpr bool use_lane_kernel() {
     return TGMS_LANE_UNIFORM && M >= 2 && M % 2 == 0 && M <= TGMS_LANE_MAX_M;
+}
+// Even M from here up (and above the lane kernel's range) take the joint lane-pair solve
+// with whole-line output (k_reduced_uniform_lines).
+#ifndef TGMS_PAIR_LINES_MIN_M
+#define TGMS_PAIR_LINES_MIN_M 12
+#endif
+template <int M>
+constexpr bool use_pair_lines() {
+    return !use_lane_kernel<M>() && M % 2 == 0 && M >= TGMS_PAIR_LINES_MIN_M && M >= 4;
 }
 
 template <int M>
@@ -2388,6 +2755,15 @@ hipError_t uniform_M(int32_t B, const double* W, const double* T, const double* 
             TGMS_LAUNCH((k_lane_uniform<M, true>), dim3(lgrid), dim3(W64), 0, stream, B, W, T, ED, C, status, nt);
         else
             TGMS_LAUNCH((k_lane_uniform<M, false>), dim3(lgrid), dim3(W64), 0, stream, B, W, T, ED, C, status, nt);
+        return hipSuccess;
+    }
+    if constexpr (use_pair_lines<M>()) {
+        if (ED)
+            TGMS_LAUNCH((k_reduced_uniform_lines<M, true>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C, status,
+                        nt);
+        else
+            TGMS_LAUNCH((k_reduced_uniform_lines<M, false>), dim3(grid), dim3(W64), 0, stream, B, W, T, ED, C,
+                        status, nt);
         return hipSuccess;
     }
     if (ED)
@@ -2485,30 +2861,40 @@ hipError_t launch_group_perm(int32_t B, const int32_t* so, const int32_t* starts
     return hipSuccess;
 }
 
-// (instantiated only for the classes a call can launch: end derivatives use the ED
-// boundary, so e.g. <1, TWO_WAVE_MAX_M, true> never exists)
-template <int MLO, int MHI, bool HAS_ED>
-hipError_t loop_multi_launch(const GroupTable& tab, const int32_t* so, const double* W, double* T, const double* ED,
-                             double kT, double eta, int32_t iters, double* cost, double* C, int32_t* status,
-                             hipStream_t stream) {
-    const unsigned grid = tab.ngroups ? (unsigned)tab.blk_end[tab.ngroups - 1] : 0u;
-    if (grid == 0) return hipSuccess;
-    if constexpr (MLO <= MHI)  // (MLO > MHI: an empty class, every M at two waves)
-        TGMS_LAUNCH((k_refine_loop_multi<MLO, MHI, HAS_ED>), dim3(grid), dim3(W64), 0, stream, tab, so, W, T, ED,
-                    kT, eta, iters, cost, C, status);
+hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int has_ed, int32_t* hist, int32_t* perm,
+                                 DevPlan* plan, int32_t* status, double* C, double* cost, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + PERM_BLOCK - 1) / PERM_BLOCK);
+    TGMS_LAUNCH(k_perm_hist, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, so, hist);
+    TGMS_LAUNCH(k_group_plan, dim3(1), dim3(PLAN_THREADS), 0, stream, n, S, so, has_ed, hist, perm, plan, status, C,
+                cost);
+    TGMS_LAUNCH(k_perm_scatter_dev, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, so, hist, plan, perm);
     return hipSuccess;
 }
 
-hipError_t launch_refine_loop_multi(int cls, const GroupTable& tab, const int32_t* so, const double* W, double* T,
-                                    const double* ED, double kT, double eta, int32_t iters, double* cost, double* C,
-                                    int32_t* status, hipStream_t stream) {
+// (instantiated only for the classes a call can launch: end derivatives use the ED
+// boundary, so e.g. <1, TWO_WAVE_MAX_M, true> never exists)
+template <int MLO, int MHI, bool HAS_ED>
+hipError_t loop_dev_launch(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W, double* T,
+                           const double* ED, double kT, double eta, int32_t iters, double* cost, double* C,
+                           int32_t* status, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if constexpr (MLO <= MHI)  // (MLO > MHI: an empty class, every M at two waves)
+        TGMS_LAUNCH((k_refine_loop_dev<MLO, MHI, HAS_ED>), dim3(dev_loop_grid(n)), dim3(W64), 0, stream, plan, cls,
+                    so, W, T, ED, kT, eta, iters, cost, C, status);
+    return hipSuccess;
+}
+
+hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+                                  double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
+                                  double* C, int32_t* status, hipStream_t stream) {
     constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
     if (ED) {
-        if (cls == 0) return loop_multi_launch<1, E, true>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
-        return loop_multi_launch<E + 1, 16, true>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+        if (cls == 0) return loop_dev_launch<1, E, true>(0, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+        return loop_dev_launch<E + 1, 16, true>(1, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
     }
-    if (cls == 0) return loop_multi_launch<1, A, false>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
-    return loop_multi_launch<A + 1, 16, false>(tab, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    if (cls == 0) return loop_dev_launch<1, A, false>(0, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+    return loop_dev_launch<A + 1, 16, false>(1, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
 }
 
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,

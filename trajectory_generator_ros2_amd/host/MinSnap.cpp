@@ -51,10 +51,14 @@ MinSnap::~MinSnap() {
 
 tgms_handle* MinSnap::handle() {
     if (!h_) {
-        const tgms_status s = tgms_create(&h_, p_.device);
+        const tgms_status s = p_.host_backend ? tgms_create_host(&h_) : tgms_create(&h_, p_.device);
         if (s != TGMS_OK) {
             h_ = nullptr;
-            log_error("MinSnap: cannot create the GPU solver on device %d: %s", p_.device, tgms_status_string(s));
+            if (p_.host_backend)
+                log_error("MinSnap: cannot create the host solver: %s", tgms_status_string(s));
+            else
+                log_error("MinSnap: cannot create the GPU solver on device %d: %s", p_.device,
+                          tgms_status_string(s));
         }
     }
     return h_;
@@ -64,7 +68,7 @@ bool MinSnap::solve_and_sample(const std::vector<double>& W, const std::vector<d
                                std::vector<double>& coeffs, std::vector<double>& samples, std::string& err) {
     tgms_handle* h = handle();
     if (!h) {
-        err = "no GPU solver";
+        err = p_.host_backend ? "no host solver" : "no GPU solver";
         return false;
     }
     const int32_t M = (int32_t)T.size();

@@ -4,8 +4,9 @@
 // It is one more trajectory next to Circle / Line / Figure8 ... (reference
 // include/trajectory_generator_ros2/trajectories/*.hpp), built by the traj_type
 // factory branch "MinSnap" (factory.hpp, mirrors src/TrajectoryGenerator.cpp:175-388).
-// Every solve and every sample runs on the GPU through the C ABI (include/tgms.h);
-// there is no CPU path.
+// Every solve and every sample runs on the GPU through the C ABI (include/tgms.h),
+// unless the node's YAML asks for the host backend (`minsnap_backend: host`, config 1: a
+// node with no GPU); there is no silent CPU fallback.
 //
 //   generateTraj            tgms_solve_batch (B = 1, rest-to-rest) + tgms_sample_batch at dt,
 //                           appended to goals (Line.cpp:33-89 append convention)
@@ -32,6 +33,8 @@ struct MinSnapParams {
     double yaw = 0.0;               // psi for TGMS_YAW_CONSTANT (and at rest)
     double stop_accel = 1.0;        // braking deceleration for generateStopTraj [m/s^2]
     int device = 0;                 // HIP device ordinal
+    bool host_backend = false;      // `minsnap_backend: host`: the explicit CPU backend (config 1,
+                                    // a node with no GPU; tgms_create_host), never a fallback
 };
 
 class MinSnap : public Trajectory {

@@ -172,6 +172,13 @@ bool readMinSnapParameters(Node& node, double dt, std::unique_ptr<Trajectory>& t
     double device = 0;
     node.get_parameter("device", device);
     p.device = (int)device;
+    std::string backend = "hip";  // "host": the explicit CPU backend for a node with no GPU (config 1)
+    node.get_parameter("minsnap_backend", backend);
+    if (backend != "hip" && backend != "host") {
+        log_error("minsnap_backend must be \"hip\" or \"host\"");
+        return false;
+    }
+    p.host_backend = backend == "host";
     traj = std::make_unique<MinSnap>(p, dt);
     return true;
 }

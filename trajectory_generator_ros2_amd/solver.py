@@ -28,14 +28,19 @@ def _ptr(a) -> Optional[int]:
 
 
 class Solver:
-    """A libtgms handle bound to one HIP device."""
+    """A libtgms handle bound to one HIP device (or, asked for explicitly, the host backend)."""
 
-    def __init__(self, device: int = 0, method: int = _lib.METHOD_REDUCED, device_count: int = 0):
+    def __init__(self, device: int = 0, method: int = _lib.METHOD_REDUCED, device_count: int = 0,
+                 host: bool = False):
         """device_count > 0: a multi-GPU handle over devices 0..device_count-1
-        (tgms_create_multi: one RCCL communicator per device); else one device."""
+        (tgms_create_multi: one RCCL communicator per device); host=True: the explicit host
+        backend (tgms_create_host: solve + sample on the CPU, config 1); else one device."""
         self._L = _lib.load()
         h = ctypes.c_void_p()
-        if device_count > 0:
+        if host:
+            st = self._L.tgms_create_host(ctypes.byref(h))
+            what = "tgms_create_host"
+        elif device_count > 0:
             st = self._L.tgms_create_multi(ctypes.byref(h), int(device_count))
             what = "tgms_create_multi"
         else:
