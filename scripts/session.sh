@@ -8,6 +8,7 @@
 # STEP is one of
 #   smoke                      __graft_entry__.smoke()
 #   tests[:K_EXPR]             pytest -m gpu (optionally -k K_EXPR)
+#   testsall                   pytest -m gpu without -x (every failure in one run)
 #   bench                      the headline bench line (bench.json)
 #   prof                       rocprofv3 --kernel-trace --stats: headline alone, then every side line
 #   pmc                        PMC traffic passes of the headline (scripts/gpu_profile.sh)
@@ -60,6 +61,11 @@ for step in "$@"; do
         log="$OUT/pytest_gpu${a:+_$(echo "$a" | tr -c 'a-zA-Z0-9_\n' '_')}.log"
         pytest_gpu "$log" "${a:-}"; rc=$?
         tail -3 "$log"
+        [ $rc -eq 0 ] || end "$step" $rc ;;
+    testsall)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+            > "$OUT/pytest_gpu_all.log" 2>&1; rc=$?
+        tail -15 "$OUT/pytest_gpu_all.log"
         [ $rc -eq 0 ] || end "$step" $rc ;;
     vtests)
         log="$OUT/pytest_gpu_$a.log"

@@ -192,8 +192,7 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 // This lane's index in its wavefront, recomputed where it is used (volatile: never hoisted
-// or kept live across the sweep).  Used by the back substitution only: see the group loop
-// for the forward sweep's index.
+// or kept live across the sweep).  Used by the back substitution only (see the group loop).
 __device__ __forceinline__ int lane_now() {
     int l = 0;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "+v"(l));
@@ -501,12 +500,18 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         scratch + (size_t)wave_id * QTW * N * SW, (short)0, QTW * N * SW * 8, 0x00020000);
     const int ngroups = (n_traj + QTW - 1) / QTW;
 
-    // The forward sweep's lane index from threadIdx.x (a value the compiler can range): taken
-    // from an inline-asm v_mbcnt at the top of each group instead (lane_now), the trajectories
-    // of quads 3, 7, 11 and 15 of a wave's second and later groups came out wrong with status
-    // OK (round 5, scripts/band_diag.py at M = 3 x 20,001: 160-251 of 20,001 wrong in every
-    // run; the same kernel with this line exact, A/B on one box, gpurun_out r05e); a wait for
-    // the previous group's memory traffic at the top of the group did not change it.
+    // The forward sweep's lane index from threadIdx.x, computed once, and the trajectory's
+    // LDS block and slab places from it once per group.  Round 5: every build that derived
+    // them otherwise -- the index by an inline-asm v_mbcnt or by the mbcnt builtins at the top
+    // of each group (no scratch at any M), the places re-derived from the index in every step,
+    // or only the two single-slot store offsets re-derived per step from vrow and q (scratch
+    // at 3 of 32 M each) -- gave wrong trajectories with status OK: quads 3, 7, 11
+    // and 15 (DPP bank 3 of every row) of about a third of a wave's second and later groups,
+    // varying run to run: the signature of round 3's unexplained two-wave failure (DESIGN.md
+    // section 4).  scripts/band_diag.py at M = 3 x 20,001: 160-267 wrong per run; a memory
+    // wait at the top of the group did not change it; this form: none in every run and every
+    // band test (gpurun_out r05e-r05h).  The cause is not identified (the ISA shows no DPP,
+    // EXEC or waitcnt hazard we could find); tests/test_gpu_band.py's round-3 shapes catch it.
     const int lane_top = threadIdx.x % W64;
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
         const int lane = lane_top, g = lane / QL;

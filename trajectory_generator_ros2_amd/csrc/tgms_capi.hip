@@ -6,6 +6,8 @@
 // MinSnap adapter maps a failure to the reference's RCLCPP_ERROR + exit(1)
 // (Line.cpp:77-78).  There is deliberately NO CPU fallback: without a HIP
 // device tgms_create() fails with TGMS_ERR_NO_DEVICE.
+#include <chrono>
+#include <thread>
 #include <initializer_list>
 #include "tgms.h"
 #include "tgms_internal.h"
@@ -102,6 +104,13 @@ struct tgms_handle {
     double* d_band_graph = nullptr;
     size_t band_graph_cap = 0;
     std::vector<double*> band_retired;
+    // Completion marker of the uncaptured band-KKT calls, for a capture that takes d_band
+    // over: each uncaptured band call's scratch_release writes band_seq into this pinned word
+    // from its stream (hipStreamWriteValue32); the hand-off waits on the host until the word
+    // reaches the last value issued -- no HIP call, so the caller's capture stays valid.
+    uint32_t* band_done = nullptr;  // pinned, mapped
+    uint32_t band_seq = 0;
+    bool band_unmarked = false;  // an uncaptured band call since the last marker
 };
 
 namespace {
@@ -157,6 +166,10 @@ tgms_status scratch_release(tgms_handle* h, hipStream_t stream) {
     if (capturing(stream)) return TGMS_OK;
     TGMS_HIP(h, hipEventRecord(h->scratch_ev, stream));
     h->scratch_pending = true;
+    if (h->band_unmarked) {
+        TGMS_HIP(h, hipStreamWriteValue32(stream, h->band_done, ++h->band_seq, 0));
+        h->band_unmarked = false;
+    }
     return TGMS_OK;
 }
 
@@ -468,17 +481,17 @@ tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream, double** 
             if (!(h->d_band && need <= h->band_cap))
                 return no_capture(h, stream, "a band-KKT call that grows the handle's slab");
             // An uncaptured call may still be running on that slab (on any stream): nothing
-            // orders the graphs' replays after it, so the host waits for it here.  The
-            // handle's event was recorded outside any capture, which a thread-local capture
-            // lets the host wait on; where the caller's capture mode forbids the wait, the
-            // call refuses instead of handing over a slab that is still in use.
-            if (h->scratch_pending) {
-                if (hipEventSynchronize(h->scratch_ev) != hipSuccess)
-                    return set_err(h, TGMS_ERR_UNSUPPORTED,
-                                   "a band-KKT capture would take over the handle's slab while an uncaptured "
-                                   "call may still use it; synchronize before capturing, or capture with "
-                                   "hipStreamCaptureModeThreadLocal");
-                h->scratch_pending = false;
+            // orders the graphs' replays after it, so the host waits for it here -- on the
+            // pinned completion word, not a HIP call (hipEventSynchronize inside a capture
+            // invalidates it, round 5)
+            if (h->band_done) {
+                const auto t0 = std::chrono::steady_clock::now();
+                while ((int32_t)(__atomic_load_n(h->band_done, __ATOMIC_ACQUIRE) - h->band_seq) < 0) {
+                    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                        return set_err(h, TGMS_ERR_DEVICE,
+                                       "a band-KKT capture waited 60 s for an uncaptured call on the slab it takes over");
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                }
             }
             if (h->d_band_graph) h->band_retired.push_back(h->d_band_graph);  // an older graph may use it
             h->d_band_graph = h->d_band;
@@ -489,6 +502,12 @@ tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream, double** 
         *slab = h->d_band_graph;
         return TGMS_OK;
     }
+    if (!h->band_done) {
+        TGMS_HIP(h, hipHostMalloc(reinterpret_cast<void**>(&h->band_done), sizeof(uint32_t),
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+        *h->band_done = h->band_seq;
+    }
+    h->band_unmarked = true;  // this call's release writes the marker
     if (need > h->band_cap) {
         if (h->d_band) {
             TGMS_HIP(h, hipStreamSynchronize(stream));
@@ -1265,6 +1284,7 @@ void tgms_destroy(tgms_handle* h) {
     if (h->h_perm) (void)hipHostFree(h->h_perm);
     if (h->perm_ev) (void)hipEventDestroy(h->perm_ev);
     if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
+    if (h->band_done) (void)hipHostFree(h->band_done);
     if (h->d_loop_ws) (void)hipFree(h->d_loop_ws);
     for (int j = 0; j < TGMS_AUX_STREAMS; ++j) {
         if (h->aux[j]) (void)hipStreamDestroy(h->aux[j]);
