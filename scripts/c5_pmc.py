@@ -4,8 +4,8 @@ into profiles/c5_pmc.json: per tgms_refine_loop_device call of bench.py's config
 share, the executed FP64 flops (64 lanes x (ADD + MUL + 2 FMA)), VALU instructions and
 HBM bytes (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE, MI355X_MICROARCH.md), summed over
 the two occupancy-class kernels that one call launches.
-    python3 scripts/c5_pmc.py gpurun_out/c5pmc_d [profiles/c5_pmc.json]"""
-import collections, csv, glob, json, sys
+    python3 scripts/c5_pmc.py gpurun_out/r05k/pmc_c5bench_default [profiles/c5_pmc.json]"""
+import collections, csv, glob, json, re, sys
 
 src = sys.argv[1]
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/c5_pmc.json"
@@ -13,11 +13,10 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{src}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "k_refine_loop_multi" not in k:
+        m = re.search(r"(k_refine_loop_(?:multi|dev))<(\d+), (\d+)", k)
+        if not m:
             continue
-        import re
-        m = re.search(r"k_refine_loop_multi<(\d+), (\d+)", k)
-        cls = f"k_refine_loop_multi<{m.group(1)},{m.group(2)}>" if m else "k_refine_loop_multi"
+        cls = f"{m.group(1)}<{m.group(2)},{m.group(3)}>"
         acc[cls][r["Counter_Name"]].append(float(r["Counter_Value"]))
 kern = {c: {n: sum(v) / len(v) for n, v in d.items()} for c, d in acc.items()}
 tot = collections.Counter()

@@ -9,13 +9,14 @@ import collections
 import csv
 import glob
 import os
+import re
 import sys
 
 d = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0]
+        name = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).split("(")[0]
         if name.startswith("__amd") or "elementwise" in name or "at::" in name:
             continue
         acc[(name, r["Counter_Name"])].append(float(r["Counter_Value"]))
