@@ -276,3 +276,42 @@ def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
     np.testing.assert_array_equal(T1[segs_bad], T[segs_bad])
     assert np.isfinite(C[~segs_bad]).all() and (cost[~bad] > 0).all()
     assert not np.array_equal(T1[~segs_bad], T[~segs_bad])
+
+
+@pytest.mark.parametrize("with_ed", [False, True])
+def test_refine_multi_uniform_batch_takes_the_device_grouped_loop(oracle, with_ed):
+    """Round 5: tgms_refine_loop_multi_device runs every batch, uniform ones too, through the
+    device-grouped fused loop (the host no longer scans the offsets to detect uniformity).
+    A uniform batch through the RCCL pipeline (self-gather) against the oracle: times and
+    costs after 10 steps at the loop's amplification tolerance (as
+    the configs' refinement tests), the final coefficients at north_star's 1e-9 on the GPU's
+    own times.  Tolerance after 10 steps: 1e-7, as test_gpu_configs.py's refinement tests
+    (the iterated map amplifies rounding; measured 1.3e-8 here, round 5)."""
+    import torch
+    from conftest import batch_rel_err
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(3001, 10, seed=71)
+    W, T = W.reshape(-1, 3), T.reshape(-1)
+    B, Sg = len(so) - 1, int(so[-1])
+    ED = np.random.default_rng(72).normal(scale=0.3, size=(B, 18)) if with_ed else None
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so.astype(np.int32)), d(W), d(T.copy())
+    dED = d(ED) if with_ed else None
+    dC = torch.full((Sg, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+    dcost = torch.full((B,), float("nan"), dtype=torch.float64, device="cuda")
+    dst = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    mh = _self_gather_handle()
+    try:
+        mh.refine_loop_multi_device(so, dso, dW, dT, 1.0, 0.1, 10, dC, dcost, dst, d_end_derivs=dED)
+        torch.cuda.synchronize()
+    finally:
+        mh.close()
+    assert int(dst.abs().sum()) == 0
+    Tg, Cg, cg = dT.cpu().numpy(), dC.cpu().numpy(), dcost.cpu().numpy()
+    To, co, Co, sto = oracle.refine_batch(so, W, T, ED, 1.0, 0.1, 10, oracle.REDUCED)
+    assert (sto == 0).all()
+    assert np.abs(Tg / To - 1).max() <= 1e-7
+    assert np.abs(cg / co - 1).max() <= 1e-7
+    R, rst = oracle.solve_batch(so, W, Tg, ED, oracle.REDUCED)
+    assert (rst == 0).all()
+    assert batch_rel_err(so, Cg, R) <= 1e-9

@@ -5,13 +5,11 @@ trajectory_generator_ros2_amd/build/, unbundled, `llvm-readelf --notes`).
 VERDICT r04 items 1, 3 and 4 asked for no scratch in the refinement loops, in every kernel a
 uniform solve launches and in the band-KKT kernel at two wavefronts per SIMD.  Round 5: every
 kernel of the library runs without scratch memory (a VGPR "spill" of the one-wave
-refinement classes goes to AGPRs, counted but not scratch) except 11 of the 32 band-KKT
-instantiations, which keep 1-4 VGPRs (8-20 B) in scratch, 17 (64 B) at M = 2 with end
-derivatives (round 4: 37-94 VGPRs, 144-224 B, at every M).  The band kernel fits two
-wavefronts per SIMD (<= 256 VGPRs, no AGPRs).  Every build of it with less scratch that
-round 5 tried re-derived lane-dependent values inside the group loop and gave wrong results
-on the GPU (csrc/tgms_band.hip, the group loop's comment); this test pins the shipped form's
-budget, instantiation by instantiation."""
+refinement classes goes to AGPRs, counted but not scratch) except three of the 32 band-KKT
+instantiations, which keep one VGPR (8 B) in scratch: M = 2 and 9 with end derivatives, M = 7
+without (round 4: 37-94 VGPRs, 144-224 B, at every M).  The band kernel fits two wavefronts
+per SIMD (<= 256 VGPRs, no AGPRs).  This test pins that budget instantiation by
+instantiation (csrc/tgms_band.hip: the builds with less scratch were wrong on the GPU)."""
 import os
 import re
 import shutil
@@ -22,9 +20,7 @@ import pytest
 LLVM = "/opt/rocm/lib/llvm/bin"
 SOURCES = ["tgms_reduced", "tgms_band", "tgms_dense", "tgms_sample"]
 # (M, HAS_ED) -> (VGPRs spilled, scratch bytes) of the band instantiations that spill
-BAND_SPILL = {(2, True): (17, 64), (2, False): (1, 8), (5, True): (2, 12), (5, False): (2, 12), (7, False): (4, 20),
-              (9, True): (2, 12), (9, False): (2, 12), (12, True): (2, 12), (12, False): (2, 12), (16, True): (2, 12),
-              (16, False): (2, 12)}
+BAND_SPILL = {(2, True): (1, 8), (7, False): (1, 8), (9, True): (1, 8)}
 
 
 def _kernels(tmp_path, src):

@@ -282,7 +282,7 @@ typedef int (&PosRef)[WR];
 template <int M, bool HAS_ED, int R>
 __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)[WR][NJ], PosRef P,
                                           int& sing, __amdgpu_buffer_rsrc_t rs, const uint32_t vrow,
-                                          const uint32_t vrow1, const uint32_t vrow5, const int* sd, double* X) {
+                                          const int* sd, double* X) {
     constexpr int N = 14 * M + 2;
     constexpr int JR = R / 4, O = R % 4;
     constexpr int BC = O * 0x55;        // quad_perm [O, O, O, O]
@@ -344,6 +344,20 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         for (int j = 0; j < NJ; ++j) v[j] = (j == JR && q == O) ? 0.0 : p[j] * inv;
 #ifndef TGMS_BAND_NOSTORE  // ablation build: no slab stores
         const int so = k * (SW * 8);
+        // this lane's singles at 128 + 8 q and (register 5: the right-hand sides 1 and 2,
+        // lanes 0 and 1; lanes 2 and 3 hold the unused slots 22 and 23, which the slab does
+        // not keep: an out-of-range offset drops the store) 160 + 8 q, re-derived here so no
+        // register holds them over the sweep.  Store-offset hazard (round 5): a buffer store
+        // whose voffset a VALU instruction wrote three instructions earlier stored some lanes
+        // at a stale offset (wrong trajectories in DPP bank 3 of later groups, 128-144 of
+        // 20,001 per run at M = 3); 16 wait states between the two are exact in every run and
+        // shape (profiles/r05_band_lane_variants.jsonl, variants L / LN).
+        const uint32_t vrow1 = vrow + 128u - 8u * (uint32_t)q;
+        const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
+        asm volatile("" ::"v"(vrow1), "v"(vrow5));
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[0], v[2])), rs, vrow, so, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[1], v[3])), rs, vrow + 64u, so, 0);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[4]), rs, vrow1, so, 0);
@@ -501,28 +515,25 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     const int ngroups = (n_traj + QTW - 1) / QTW;
 
     // The forward sweep's lane index from threadIdx.x, computed once, and the trajectory's
-    // LDS block and slab places from it once per group.  Round 5: every build that derived
+    // LDS block and pair-slot place from it once per group.  Round 5: the builds that derived
     // them otherwise -- the index by an inline-asm v_mbcnt or by the mbcnt builtins at the top
     // of each group (no scratch at any M), the places re-derived from the index in every step,
-    // or only the two single-slot store offsets re-derived per step from vrow and q (scratch
-    // at 3 of 32 M each) -- gave wrong trajectories with status OK: quads 3, 7, 11
+    // or the two single-slot store offsets re-derived per step without the wait states in
+    // quad_step (scratch at 3 of 32 M) -- gave wrong trajectories with status OK: quads 3, 7, 11
     // and 15 (DPP bank 3 of every row) of about a third of a wave's second and later groups,
     // varying run to run: the signature of round 3's unexplained two-wave failure (DESIGN.md
     // section 4).  scripts/band_diag.py at M = 3 x 20,001: 160-267 wrong per run; a memory
     // wait at the top of the group did not change it; this form: none in every run and every
-    // band test (gpurun_out r05e-r05h).  The cause is not identified (the ISA shows no DPP,
-    // EXEC or waitcnt hazard we could find); tests/test_gpu_band.py's round-3 shapes catch it.
+    // band test (gpurun_out r05e-r05m).  For the single-slot offsets the cause is a store-offset
+    // hazard (quad_step: 16 wait states fix it); for the others it was not isolated.
+    // tests/test_gpu_band.py's round-3 shapes catch every one of them.
     const int lane_top = threadIdx.x % W64;
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
         const int lane = lane_top, g = lane / QL;
         const int q = opaque(lane % QL);
         double* const X = s_x[wv][g];
-        // this lane's places in a slab row: its pairs at 16 q (+ 64), its singles at 128 + 8 q (+ 32)
+        // this lane's place in a slab row: its pairs at 16 q (+ 64) (its singles: quad_step)
         const uint32_t vrow = (uint32_t)(g * N * SW * 8 + 16 * q);
-        const uint32_t vrow1 = (uint32_t)(g * N * SW * 8 + 128 + 8 * q);
-        // register 5: the right-hand sides 1 and 2 (lanes 0, 1); lanes 2, 3 hold the unused
-        // slots 22, 23, which the slab does not keep (an out-of-range offset drops the store)
-        const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
         const int bi = QTW * grp + g;
         const bool live = bi < n_traj;
         const int32_t b = ids ? ids[live ? bi : QTW * grp] : (live ? bi : QTW * grp);
@@ -584,7 +595,7 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         // ---- forward elimination (a3)
         for (int k0 = 0; k0 < N; k0 += WC) {
 #define STEP(R) \
-    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, P, sing, rs, vrow, vrow1, vrow5, s_desc, X);
+    if (k0 + R < N) quad_step<M, HAS_ED, R>(k0 + R, q, u, P, sing, rs, vrow, s_desc, X);
             STEP(0) STEP(1) STEP(2) STEP(3) STEP(4) STEP(5) STEP(6) STEP(7) STEP(8) STEP(9)
             STEP(10) STEP(11) STEP(12) STEP(13) STEP(14) STEP(15) STEP(16) STEP(17) STEP(18)
 #undef STEP
