@@ -216,6 +216,29 @@ def test_config3_full_size_properties(solver, oracle):
     check_spline_properties(so, W.reshape(-1, 3), T.reshape(-1), C)
 
 
+@pytest.mark.parametrize("M", [12, 13, 14, 16])
+def test_uniform_large_m_full_size_every_trajectory(solver, oracle, M):
+    """Round 5: the whole-line lane-pair kernel (even M >= 12) and the axis-sequential one
+    (odd M) at the bench's size, 65,536 trajectories, every trajectory against the oracle at
+    1e-9, over three back-to-back launches into the same buffer with different inputs (a
+    stale store offset would leave another launch's or another trajectory's values behind;
+    the band kernel's store-offset hazard)."""
+    import torch
+    from trajectory_generator_ros2_amd import synthetic as S
+    B = 65536
+    dC = torch.full((B, M, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+    dS = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    for rep in range(3):
+        so, W, T = S.uniform_batch(B, M, seed=900 + 10 * M + rep)
+        dW, dT = torch.from_numpy(W).cuda(), torch.from_numpy(T).cuda()
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS)
+        torch.cuda.synchronize()
+        assert (dS.cpu().numpy() == 0).all()
+        R, rst = oracle.solve_batch(so, W.reshape(-1, 3), T.reshape(-1), None, oracle.REDUCED)
+        assert (rst == 0).all()
+        assert batch_rel_err(so, dC.cpu().numpy().reshape(-1, 3, 8), R) <= TOL, rep
+
+
 def test_device_ragged_matches_host(solver):
     import torch
     from trajectory_generator_ros2_amd import synthetic as S
