@@ -349,9 +349,9 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         // not keep: an out-of-range offset drops the store) 160 + 8 q, re-derived here so no
         // register holds them over the sweep.  Store-offset hazard (round 5): a buffer store
         // whose voffset a VALU instruction wrote three instructions earlier stored some lanes
-        // at a stale offset (wrong trajectories in DPP bank 3 of later groups, 128-144 of
+        // at a stale offset (wrong trajectories in DPP bank 3 of later groups, 128-267 of
         // 20,001 per run at M = 3); 16 wait states between the two are exact in every run and
-        // shape (profiles/r05_band_lane_variants.jsonl, variants L / LN).
+        // shape (profiles/r05_band_lane_variants.jsonl: variants L / LN, J0 / JG).
         const uint32_t vrow1 = vrow + 128u - 8u * (uint32_t)q;
         const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
         asm volatile("" ::"v"(vrow1), "v"(vrow5));
@@ -480,6 +480,11 @@ __device__ __forceinline__ void back_step(int k, int l0, int g, __amdgpu_buffer_
         const Pos pk = decode<M>(k);
         if (pk.kind == 1 && live) {
             double* o = out + pk.seg * 24 + pk.idx;
+            // the store-offset hazard (quad_step): the address must not be a fresh VALU result
+            asm volatile("" ::"v"(o));
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
             o[0] = emit ? -sm[0] : 0.0;
             o[8] = emit ? -sm[1] : 0.0;
             o[16] = emit ? -sm[2] : 0.0;
@@ -514,22 +519,17 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
         scratch + (size_t)wave_id * QTW * N * SW, (short)0, QTW * N * SW * 8, 0x00020000);
     const int ngroups = (n_traj + QTW - 1) / QTW;
 
-    // The forward sweep's lane index from threadIdx.x, computed once, and the trajectory's
-    // LDS block and pair-slot place from it once per group.  Round 5: the builds that derived
-    // them otherwise -- the index by an inline-asm v_mbcnt or by the mbcnt builtins at the top
-    // of each group (no scratch at any M), the places re-derived from the index in every step,
-    // or the two single-slot store offsets re-derived per step without the wait states in
-    // quad_step (scratch at 3 of 32 M) -- gave wrong trajectories with status OK: quads 3, 7, 11
-    // and 15 (DPP bank 3 of every row) of about a third of a wave's second and later groups,
-    // varying run to run: the signature of round 3's unexplained two-wave failure (DESIGN.md
-    // section 4).  scripts/band_diag.py at M = 3 x 20,001: 160-267 wrong per run; a memory
-    // wait at the top of the group did not change it; this form: none in every run and every
-    // band test (gpurun_out r05e-r05m).  For the single-slot offsets the cause is a store-offset
-    // hazard (quad_step: 16 wait states fix it); for the others it was not isolated.
-    // tests/test_gpu_band.py's round-3 shapes catch every one of them.
-    const int lane_top = threadIdx.x % W64;
+    // The lane index is recomputed at the top of every group (the mbcnt builtins on an
+    // accumulator the compiler cannot hoist), so nothing lane-derived stays live across the
+    // group loop: no scratch at any M (held in a register from threadIdx.x instead, 11 of 32
+    // instantiations spilled 1-17 VGPRs).  Round 5: builds like this one returned wrong
+    // trajectories with status OK (quads 3, 7, 11, 15 of a third of a wave's later groups --
+    // round 3's unexplained signature) until the store-offset hazard was guarded: the compiler
+    // re-derived the lane-dependent slab offsets next to their buffer stores, three
+    // instructions before the store read them (quad_step).
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
-        const int lane = lane_top, g = lane / QL;
+        const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, (unsigned)opaque(0)));
+        const int g = lane / QL;
         const int q = opaque(lane % QL);
         double* const X = s_x[wv][g];
         // this lane's place in a slab row: its pairs at 16 q (+ 64) (its singles: quad_step)
