@@ -1,0 +1,107 @@
+// store_hazard.hip — does a buffer store read a VALU-written voffset correctly at every
+// distance?  (the band kernel's store-offset hazard.)
+//
+// Every lane of many waves walks its own row of `iters` 32-bit words.  Per iteration the
+// lane's offset register is advanced IN PLACE by one VALU instruction (v_add_u32 or a
+// v_cndmask_b32_e64 selecting the next offset), then D filler instructions follow (VALU
+// moves, or 16-B buffer stores to a side area with fixed offsets, as in the band kernel),
+// then buffer_store_dword writes i + 1 at the offset.  A store that read the offset's
+// previous value writes row[i - 1] twice and leaves row[i] untouched, so the host counts
+// the words that are not i + 1.  One JSON line per (filler, writer, D).
+//   hipcc --offload-arch=gfx950 -O3 -Wno-unused-value -o store_hazard store_hazard.hip && ./store_hazard
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// FILL 0: v_mov fillers; FILL 1: buffer_store_dwordx4 fillers (side area).  WR 0: v_add_u32,
+// WR 1: v_cndmask_b32_e64 (mask: lane bit 0 clear -> the next offset, else out of range).
+template <int D, int FILL, int WR>
+__global__ __launch_bounds__(256) void k_hazard(uint32_t* out, uint32_t* side, int iters) {
+    const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(gridDim.x * 256u * iters * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rside =
+        __builtin_amdgcn_make_buffer_rsrc(side, (short)0, (int)(gridDim.x * 256u * 64u), 0x00020000);
+    uint32_t off = gl * (uint32_t)iters * 4u - 4u;  // advanced before the first store
+    uint32_t nxt = off;
+    const uint32_t soff = gl * 64u;
+    const bool keep = (threadIdx.x & 1) == 0;
+    const u32x4 junk = {gl, gl, gl, gl};
+    for (int i = 0; i < iters; ++i) {
+        uint32_t val;  // i + 1 in a VGPR before the offset is written (nothing else between)
+        asm volatile("v_mov_b32 %0, %1" : "=v"(val) : "s"((uint32_t)i + 1u));
+        nxt += 4u;
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (WR == 0) {
+            asm volatile("v_add_u32_e32 %0, 4, %0" : "+v"(off));
+        } else {
+            // off = keep ? nxt : out-of-range (odd lanes store nothing)
+            asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(off) : "v"(0x7FFFFF00u), "v"(nxt), "s"(
+                             __builtin_amdgcn_ballot_w64(keep)));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FILL == 0) {
+            if constexpr (D > 0) asm volatile(".rept %c0\n\tv_mov_b32 v255, 0\n\t.endr" ::"n"(D) : "v255");
+        } else {
+#pragma unroll
+            for (int f = 0; f < D; ++f) {
+                __builtin_amdgcn_raw_buffer_store_b128(junk, rside, soff + 16u * (f & 3), 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int D, int FILL, int WR>
+void run(uint32_t* d_out, uint32_t* d_side, int blocks, int iters, std::vector<uint32_t>& h, int reps) {
+    const size_t n = (size_t)blocks * 256 * iters;
+    long bad = 0, bad_words = 0;
+    for (int r = 0; r < reps; ++r) {
+        hipMemset(d_out, 0, n * 4);
+        hipLaunchKernelGGL((k_hazard<D, FILL, WR>), dim3(blocks), dim3(256), 0, 0, d_out, d_side, iters);
+        hipDeviceSynchronize();
+        hipMemcpy(h.data(), d_out, n * 4, hipMemcpyDeviceToHost);
+        for (size_t t = 0; t < (size_t)blocks * 256; ++t) {
+            const bool keep = WR == 0 || (t & 1) == 0;
+            bool tb = false;
+            for (int i = 0; i < iters; ++i) {
+                const uint32_t want = keep ? (uint32_t)i + 1u : 0u;
+                if (h[t * iters + i] != want) {
+                    ++bad_words;
+                    tb = true;
+                }
+            }
+            bad += tb;
+        }
+    }
+    printf("{\"filler\": \"%s\", \"writer\": \"%s\", \"D\": %d, \"lanes\": %d, \"iters\": %d, \"reps\": %d, "
+           "\"lanes_with_a_wrong_word\": %ld, \"wrong_words\": %ld}\n",
+           FILL ? "buffer_store_dwordx4" : "v_mov_b32", WR ? "v_cndmask_b32_e64" : "v_add_u32", D, blocks * 256,
+           iters, reps, bad, bad_words);
+    fflush(stdout);
+}
+
+template <int FILL, int WR, int... Ds>
+void sweep(uint32_t* o, uint32_t* s, int b, int it, std::vector<uint32_t>& h, int reps) {
+    (run<Ds, FILL, WR>(o, s, b, it, h, reps), ...);
+}
+
+int main() {
+    const int blocks = 2048, iters = 64, reps = 3;  // 524,288 lanes x 64 words = 128 MB
+    uint32_t *d_out = nullptr, *d_side = nullptr;
+    hipMalloc(&d_out, (size_t)blocks * 256 * iters * 4);
+    hipMalloc(&d_side, (size_t)blocks * 256 * 64);
+    std::vector<uint32_t> h((size_t)blocks * 256 * iters);
+    sweep<0, 0, 0, 1, 2, 3, 4, 6, 8, 16>(d_out, d_side, blocks, iters, h, reps);
+    sweep<0, 1, 0, 1, 2, 3, 4, 6, 8, 16>(d_out, d_side, blocks, iters, h, reps);
+    sweep<1, 0, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
+    sweep<1, 1, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
+    hipFree(d_out);
+    hipFree(d_side);
+    return 0;
+}

@@ -222,7 +222,7 @@ def test_uniform_large_m_full_size_every_trajectory(solver, oracle, M):
     (odd M) at the bench's size, 65,536 trajectories, every trajectory against the oracle at
     1e-9, over three back-to-back launches into the same buffer with different inputs (a
     stale store offset would leave another launch's or another trajectory's values behind;
-    the band kernel's store-offset hazard)."""
+    the band kernel's store-offset failure)."""
     import torch
     from trajectory_generator_ros2_amd import synthetic as S
     B = 65536

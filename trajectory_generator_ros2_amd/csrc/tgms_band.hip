@@ -347,11 +347,12 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         // this lane's singles at 128 + 8 q and (register 5: the right-hand sides 1 and 2,
         // lanes 0 and 1; lanes 2 and 3 hold the unused slots 22 and 23, which the slab does
         // not keep: an out-of-range offset drops the store) 160 + 8 q, re-derived here so no
-        // register holds them over the sweep.  Store-offset hazard (round 5): a buffer store
-        // whose voffset a VALU instruction wrote three instructions earlier stored some lanes
-        // at a stale offset (wrong trajectories in DPP bank 3 of later groups, 128-267 of
-        // 20,001 per run at M = 3); 16 wait states between the two are exact in every run and
-        // shape (profiles/r05_band_lane_variants.jsonl: variants L / LN, J0 / JG).
+        // register holds them over the sweep.  Round 5: with the stores issued three instructions
+        // after these offsets were computed, the kernel returned wrong trajectories (DPP bank 3
+        // of later groups, 128-267 of 20,001 per run at M = 3); 16 wait states between the two
+        // are exact in every run and shape (profiles/r05_band_lane_variants.jsonl: L / LN,
+        // J0 / JG).  A standalone probe of VALU-written store offsets does not reproduce the
+        // failure, so the guard stays where the kernel needs it.
         const uint32_t vrow1 = vrow + 128u - 8u * (uint32_t)q;
         const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
         asm volatile("" ::"v"(vrow1), "v"(vrow5));
@@ -480,7 +481,7 @@ __device__ __forceinline__ void back_step(int k, int l0, int g, __amdgpu_buffer_
         const Pos pk = decode<M>(k);
         if (pk.kind == 1 && live) {
             double* o = out + pk.seg * 24 + pk.idx;
-            // the store-offset hazard (quad_step): the address must not be a fresh VALU result
+            // the same guard as quad_step's slab stores: the address is not a fresh VALU result
             asm volatile("" ::"v"(o));
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -524,9 +525,9 @@ __global__ __launch_bounds__(QW * W64) __attribute__((amdgpu_waves_per_eu(TGMS_B
     // group loop: no scratch at any M (held in a register from threadIdx.x instead, 11 of 32
     // instantiations spilled 1-17 VGPRs).  Round 5: builds like this one returned wrong
     // trajectories with status OK (quads 3, 7, 11, 15 of a third of a wave's later groups --
-    // round 3's unexplained signature) until the store-offset hazard was guarded: the compiler
-    // re-derived the lane-dependent slab offsets next to their buffer stores, three
-    // instructions before the store read them (quad_step).
+    // round 3's unexplained signature) until the stores were guarded: the compiler re-derived
+    // the lane-dependent slab offsets next to their buffer stores, three instructions before
+    // the store read them (quad_step).
     for (int grp = wave_id; grp < ngroups; grp += gridDim.x * QW) {
         const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, (unsigned)opaque(0)));
         const int g = lane / QL;

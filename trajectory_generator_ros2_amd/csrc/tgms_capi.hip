@@ -1277,6 +1277,7 @@ void tgms_destroy(tgms_handle* h) {
     (void)hipDeviceSynchronize();
     if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->d_perm_hist) (void)hipFree(h->d_perm_hist);
+    if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_band) (void)hipFree(h->d_band);
     if (h->d_band_graph) (void)hipFree(h->d_band_graph);
     for (double* p : h->band_retired) (void)hipFree(p);
