@@ -2,7 +2,8 @@
 """Config 5, one GPU's share (bench.py's config5 line: shard 0 of 8 of the 1,048,576
 ragged batch, M ~ U{2..16}): K calls of tgms_refine_loop_device (10 steps + cost +
 final solve), timed with HIP events around each call on the launch stream (GPU time)
-and by wall clock (host planning included).  C5_B overrides the global batch size."""
+and by wall clock (host planning included).  C5_B overrides the global batch size; C5_MSEL=lo-hi keeps only the shard's trajectories
+with lo <= M <= hi (one occupancy class timed alone on the same trajectories)."""
 import json, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -17,6 +18,14 @@ so_all, W_all, T_all = S.ragged_batch(Bt, 2, 16)
 bounds = SH.ragged_bounds(so_all, 8)
 so, W, T, _ = SH.shard_csr(so_all, W_all, T_all, None, int(bounds[0]), int(bounds[1]))
 so = so.astype(np.int32)
+if os.environ.get("C5_MSEL"):  # "lo-hi": keep only this shard's trajectories with lo <= M <= hi
+    mlo, mhi = (int(x) for x in os.environ["C5_MSEL"].split("-"))
+    Ms = np.diff(so)
+    keep = np.nonzero((Ms >= mlo) & (Ms <= mhi))[0]
+    Wr = np.asarray(W).reshape(-1, 3)
+    W = np.concatenate([Wr[so[i] + i:so[i + 1] + i + 1] for i in keep])
+    T = np.concatenate([T[so[i]:so[i + 1]] for i in keep])
+    so = np.concatenate([[0], np.cumsum(Ms[keep])]).astype(np.int32)
 B = len(so) - 1
 s = Solver(0)
 d_so = torch.from_numpy(so).cuda()

@@ -17,7 +17,9 @@
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // FILL 0: v_mov fillers; FILL 1: buffer_store_dwordx4 fillers (side area).  WR 0: v_add_u32,
-// WR 1: v_cndmask_b32_e64 (mask: lane bit 0 clear -> the next offset, else out of range).
+// WR 1: v_cndmask_b32_e64 (mask: lane bit 0 clear -> the next offset, else out of range),
+// WR 2: the band step's shape (fresh offset, VALU compare -> SGPR mask, FP64 work, in-place
+// select of the offset or out of range for lanes with q = lane & 3 >= 2).
 template <int D, int FILL, int WR>
 __global__ __launch_bounds__(256) void k_hazard(uint32_t* out, uint32_t* side, int iters) {
     const uint32_t gl = blockIdx.x * 256 + threadIdx.x;
@@ -30,12 +32,28 @@ __global__ __launch_bounds__(256) void k_hazard(uint32_t* out, uint32_t* side, i
     const uint32_t soff = gl * 64u;
     const bool keep = (threadIdx.x & 1) == 0;
     const u32x4 junk = {gl, gl, gl, gl};
+    const uint32_t q = threadIdx.x & 3;
+    double fp = 1.0;
     for (int i = 0; i < iters; ++i) {
         uint32_t val;  // i + 1 in a VGPR before the offset is written (nothing else between)
         asm volatile("v_mov_b32 %0, %1" : "=v"(val) : "s"((uint32_t)i + 1u));
         nxt += 4u;
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (WR == 0) {
+        if constexpr (WR == 2) {
+            // the band step's shape: the offset written fresh, a VALU compare writing the SGPR
+            // mask (lane bits 0-1: q < 2 keeps the offset), FP64 work, the select in place
+            uint64_t m;
+            asm volatile(
+                "v_add_u32_e32 %0, 0, %3\n\t"
+                "v_cmp_gt_u32_e64 %1, 2, %4\n\t"
+                "v_mul_f64 %2, %2, %2\n\t"
+                "v_mul_f64 %2, %2, %2\n\t"
+                "v_mul_f64 %2, %2, %2\n\t"
+                "v_mul_f64 %2, %2, %2\n\t"
+                "v_cndmask_b32_e64 %0, %5, %0, %1"
+                : "=&v"(off), "=&s"(m), "+v"(fp)
+                : "v"(nxt), "v"(q), "v"(0x7FFFFF00u));
+        } else if constexpr (WR == 0) {
             asm volatile("v_add_u32_e32 %0, 4, %0" : "+v"(off));
         } else {
             // off = keep ? nxt : out-of-range (odd lanes store nothing)
@@ -55,6 +73,7 @@ __global__ __launch_bounds__(256) void k_hazard(uint32_t* out, uint32_t* side, i
         __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
+    if (fp == 12345.0) out[0] = 0;  // keeps the FP64 filler alive
 }
 
 template <int D, int FILL, int WR>
@@ -67,7 +86,7 @@ void run(uint32_t* d_out, uint32_t* d_side, int blocks, int iters, std::vector<u
         hipDeviceSynchronize();
         hipMemcpy(h.data(), d_out, n * 4, hipMemcpyDeviceToHost);
         for (size_t t = 0; t < (size_t)blocks * 256; ++t) {
-            const bool keep = WR == 0 || (t & 1) == 0;
+            const bool keep = WR == 0 || (WR == 1 && (t & 1) == 0) || (WR == 2 && (t & 3) < 2);
             bool tb = false;
             for (int i = 0; i < iters; ++i) {
                 const uint32_t want = keep ? (uint32_t)i + 1u : 0u;
@@ -81,7 +100,7 @@ void run(uint32_t* d_out, uint32_t* d_side, int blocks, int iters, std::vector<u
     }
     printf("{\"filler\": \"%s\", \"writer\": \"%s\", \"D\": %d, \"lanes\": %d, \"iters\": %d, \"reps\": %d, "
            "\"lanes_with_a_wrong_word\": %ld, \"wrong_words\": %ld}\n",
-           FILL ? "buffer_store_dwordx4" : "v_mov_b32", WR ? "v_cndmask_b32_e64" : "v_add_u32", D, blocks * 256,
+           FILL ? "buffer_store_dwordx4" : "v_mov_b32", WR == 2 ? "band_step" : (WR ? "v_cndmask_b32_e64" : "v_add_u32"), D, blocks * 256,
            iters, reps, bad, bad_words);
     fflush(stdout);
 }
@@ -101,6 +120,8 @@ int main() {
     sweep<0, 1, 0, 1, 2, 3, 4, 6, 8, 16>(d_out, d_side, blocks, iters, h, reps);
     sweep<1, 0, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
     sweep<1, 1, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
+    sweep<0, 2, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
+    sweep<1, 2, 0, 1, 2, 3, 4, 6, 8>(d_out, d_side, blocks, iters, h, reps);
     hipFree(d_out);
     hipFree(d_side);
     return 0;

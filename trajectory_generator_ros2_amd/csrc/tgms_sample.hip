@@ -22,6 +22,9 @@
 namespace tgms {
 namespace {
 
+#ifndef TGMS_SAMPLE_NT
+#define TGMS_SAMPLE_NT 0
+#endif
 constexpr int SW = 4;                  // wavefronts per workgroup
 constexpr int G = TGMS_GOAL_STRIDE;    // 14 doubles per sample
 constexpr int CH = W64 * G / 2;        // double2 per wave chunk (448)
@@ -167,7 +170,15 @@ __global__ __launch_bounds__(W64 * SW) void k_sample(int32_t B, const int32_t* _
 #pragma unroll
             for (int q = 0; q < G / 2; ++q) {
                 const int idx = q * W64 + lane;
+#if TGMS_SAMPLE_NT  // nontemporal stores: 0.61 against 0.50 ms (profiles/r05_sampler_nt_ab.jsonl), off
+                if (idx < n2) {
+                    typedef double d2v __attribute__((ext_vector_type(2)));
+                    const double2 x = st2[idx];
+                    __builtin_nontemporal_store(d2v{x.x, x.y}, reinterpret_cast<d2v*>(&dst[idx]));
+                }
+#else
                 if (idx < n2) dst[idx] = st2[idx];
+#endif
             }
             __builtin_amdgcn_wave_barrier();
         }
