@@ -315,3 +315,35 @@ def test_refine_multi_uniform_batch_takes_the_device_grouped_loop(oracle, with_e
     R, rst = oracle.solve_batch(so, W, Tg, ED, oracle.REDUCED)
     assert (rst == 0).all()
     assert batch_rel_err(so, Cg, R) <= 1e-9
+
+
+@pytest.mark.parametrize("device_count", [0, 1], ids=["single", "multi"])
+def test_destroy_leaves_no_stale_hip_error(device_count):
+    """tgms_destroy frees each buffer once and leaves no HIP error behind for the caller's
+    next HIP call (hipGetLastError is per thread, and torch checks it after every launch).
+    A double free of the device plan once made the next test's torch.full raise
+    hipErrorInvalidValue right after a handle that had run a refinement loop was closed."""
+    import torch
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver
+    so, W, T = S.ragged_batch(2001, 2, 16, seed=44)
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    B, Sg = len(so) - 1, int(so[-1])
+    s = Solver(device_count=device_count) if device_count else Solver(0)
+    dso, dW, dT = d(so.astype(np.int32)), d(W), d(T.copy())
+    dC = torch.empty((Sg, 3, 8), dtype=torch.float64, device="cuda")
+    dcost = torch.empty((B,), dtype=torch.float64, device="cuda")
+    dst = torch.empty((B,), dtype=torch.int32, device="cuda")
+    loop = s.refine_loop_multi_device if device_count else s.refine_loop_device
+    loop(so, dso, dW, dT, 1.0, 0.1, 3, dC, dcost, dst)  # the device plan, the loop graph
+    torch.cuda.synchronize()
+    assert int((dst != 0).sum()) == 0
+    if not device_count:
+        s.set_method(METHOD_BAND_KKT)  # the band slabs and the completion word
+        _, st, _ = s.solve(so, W, T)
+        assert (st == 0).all()
+    s.close()
+    x = torch.full((1024,), 2.0, dtype=torch.float64, device="cuda")  # raised before the fix
+    torch.cuda.synchronize()
+    assert float(x.sum()) == 2048.0

@@ -1277,7 +1277,6 @@ void tgms_destroy(tgms_handle* h) {
     (void)hipDeviceSynchronize();
     if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->d_perm_hist) (void)hipFree(h->d_perm_hist);
-    if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->d_band) (void)hipFree(h->d_band);
     if (h->d_band_graph) (void)hipFree(h->d_band_graph);
     for (double* p : h->band_retired) (void)hipFree(p);
@@ -1297,6 +1296,9 @@ void tgms_destroy(tgms_handle* h) {
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    // destroy reports nothing: leave no error of these calls behind for the caller's next
+    // HIP call to pick up (hipGetLastError is per thread)
+    (void)hipGetLastError();
     delete h;
 }
 

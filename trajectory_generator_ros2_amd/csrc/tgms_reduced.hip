@@ -41,11 +41,14 @@ namespace {
 // The axis-sequential lane-pair solve reads the next knot's waypoints and 1/T from the
 // LDS stage one step ahead (the per-step SCHED_FENCE otherwise exposes the LDS latency at
 // every step): config 5 0.477-0.488 -> 0.462-0.473 ms, uniform M = 3/5 -2-3 % (round 4).
+// The joint solve does the same (TGMS_JOINT_PREFETCH): the one-wave class timed alone
+// 0.232-0.233 -> 0.216-0.220 ms, the whole config-5 call 0.486-0.492 -> 0.477-0.485 ms,
+// three alternating runs (round 5, profiles/r05_c5_joint_prefetch_ab.jsonl).
 #ifndef TGMS_PAIR_PREFETCH
 #define TGMS_PAIR_PREFETCH 1
 #endif
 #ifndef TGMS_JOINT_PREFETCH
-#define TGMS_JOINT_PREFETCH 0
+#define TGMS_JOINT_PREFETCH 1
 #endif
 #ifndef TGMS_JOINT_AXES
 #define TGMS_JOINT_AXES 1
@@ -90,11 +93,41 @@ constexpr int PSTRIDE = 33;  // LDS row stride (doubles) of the [field][trajecto
 // the 8 lanes of each ds_write_b128 group hit 8 distinct 4-bank slots.
 constexpr int OSTRIDE = 10;
 
+// The one-wave (joint-axes, M > TGMS_TWO_WAVE_MAX_M) kernels read the stage with no second
+// wavefront to hide LDS time, and with the padded stride the two lanes of a pair collide:
+// a ds_read_b64 serves lanes 0-31 and 32-63 in one LDS cycle each, i.e. 16 trajectories
+// whose even lanes read knot j and odd lanes knot M-j, two 32-bank windows at a distance
+// of 2 (F_e - F_o) banks that overlap for almost every j (PMC of the one-wave class alone:
+// SQ_LDS_BANK_CONFLICT 2.1x SQ_ACTIVE_INST_LDS).  Swizzled: rows of exactly 32 doubles, and
+// the rows of the second half of the trajectory (knot k with 2k > M, segment i with
+// 2i + 1 > M) hold trajectory t at column t ^ 16, so in every read the pair's two lanes
+// land in opposite bank halves (the middle knot / segment both read is one address).
+#ifndef TGMS_PAIR_SWIZZLE
+#define TGMS_PAIR_SWIZZLE 1
+#endif
+#ifndef TGMS_PAIR_SWIZZLE_MIN_M
+#define TGMS_PAIR_SWIZZLE_MIN_M (TGMS_TWO_WAVE_MAX_M + 1)
+#endif
+template <int M>
+constexpr bool pair_swz() { return TGMS_PAIR_SWIZZLE && M >= TGMS_PAIR_SWIZZLE_MIN_M; }
+template <int M>
+constexpr int pstride() { return pair_swz<M>() ? TPW : PSTRIDE; }
+template <int M>
+__device__ __forceinline__ int w_at(int q, int t) {  // field q = 3 knot + axis, trajectory t
+    if constexpr (pair_swz<M>()) return q * TPW + ((2 * (q / 3) > M) ? (t ^ 16) : t);
+    else return q * PSTRIDE + t;
+}
+template <int M>
+__device__ __forceinline__ int r_at(int i, int t) {  // segment i, trajectory t
+    if constexpr (pair_swz<M>()) return i * TPW + ((2 * i + 1 > M) ? (t ^ 16) : t);
+    else return i * PSTRIDE + t;
+}
+
 // One group's staged inputs, [field][trajectory] with a padded trajectory stride.
 template <int M>
 struct In {
-    double W[(M + 1) * 3 * PSTRIDE];
-    double R[M * PSTRIDE];  // 1/T, computed once while staging (T itself is not staged:
+    double W[(M + 1) * 3 * pstride<M>()];
+    double R[M * pstride<M>()];  // 1/T, computed once while staging (T itself is not staged:
                             // at 2.9 KB for M = 11 it cost the 2-wave kernels their 8th wave per CU)
     int64_t base[TPW];      // coefficient offset (doubles) of each slot's trajectory
     int bad[TPW];
@@ -114,23 +147,45 @@ static_assert(OSTRIDE % 2 == 0, "staged rows must keep 16-B alignment");
 // sees the trajectory as is, the odd lane time-reversed (virtual knot j = physical
 // knot M-j, virtual segment i = physical segment M-1-i).
 struct LaneView {
-    const double* Wb;  // &W[phys knot of virtual knot 0][axis 0][slot]
-    const double* Rb;  // &R[...]
+    const double* Wb;  // &W[phys knot of virtual knot 0][axis 0][slot] for virtual knots 2j < M
+    const double* Wf;  // the same for 2j > M and
+    const double* Wm;  // 2j == M (all three equal unless the stage is swizzled)
+    const double* Rb;  // &R[...], virtual segments 2i + 1 < M,
+    const double* Rf;  // > M and
+    const double* Rm;  // == M
     int kstep;         // +-3 fields per virtual knot (x the field stride)
     int sstep;         // +-1 segment per virtual segment (x the field stride)
-    int astep;         // doubles between the axes of one knot: PSTRIDE (transposed) or 1 (raw)
-    __device__ __forceinline__ double w(int j, int a) const { return Wb[j * kstep + a * astep]; }
-    __device__ __forceinline__ double r(int i) const { return Rb[i * sstep]; }
+    int astep;         // doubles between the axes of one knot: the field stride (transposed) or 1 (raw)
+    int m;             // M
+    __device__ __forceinline__ double w(int j, int a) const {
+        const double* p = (2 * j < m) ? Wb : ((2 * j > m) ? Wf : Wm);
+        return p[j * kstep + a * astep];
+    }
+    __device__ __forceinline__ double r(int i) const {
+        const double* p = (2 * i + 1 < m) ? Rb : ((2 * i + 1 > m) ? Rf : Rm);
+        return p[i * sstep];
+    }
 };
 
 template <int M>
 __device__ __forceinline__ LaneView make_view(const In<M>& sm, int slot, bool right) {
+    constexpr int S = pstride<M>();
     LaneView L;
-    L.Wb = sm.W + (right ? M * 3 * PSTRIDE : 0) + slot;
-    L.Rb = sm.R + (right ? (M - 1) * PSTRIDE : 0) + slot;
-    L.kstep = right ? -3 * PSTRIDE : 3 * PSTRIDE;
-    L.sstep = right ? -PSTRIDE : PSTRIDE;
-    L.astep = PSTRIDE;
+    const double* w0 = sm.W + (right ? M * 3 * S : 0);
+    const double* r0 = sm.R + (right ? (M - 1) * S : 0);
+    // swizzled: the even lane's near half (virtual = physical) is unswizzled, its far half
+    // swizzled; the odd lane (virtual knot j = physical M - j) the other way round
+    const int sx = pair_swz<M>() ? (slot ^ 16) : slot;
+    L.Wb = w0 + (right ? sx : slot);
+    L.Wf = w0 + (right ? slot : sx);
+    L.Wm = w0 + slot;
+    L.Rb = r0 + (right ? sx : slot);
+    L.Rf = r0 + (right ? slot : sx);
+    L.Rm = r0 + slot;
+    L.kstep = right ? -3 * S : 3 * S;
+    L.sstep = right ? -S : S;
+    L.astep = S;
+    L.m = M;
     return L;
 }
 
@@ -155,11 +210,12 @@ struct alignas(16) RawStage {
 template <int M>
 __device__ __forceinline__ LaneView make_view_raw(const RawIn<M>& sm, int slot, bool right) {
     LaneView L;
-    L.Wb = sm.W + slot * RawIn<M>::NW + (right ? M * 3 : 0);
-    L.Rb = sm.R + slot * M + (right ? M - 1 : 0);
+    L.Wb = L.Wf = L.Wm = sm.W + slot * RawIn<M>::NW + (right ? M * 3 : 0);
+    L.Rb = L.Rf = L.Rm = sm.R + slot * M + (right ? M - 1 : 0);
     L.kstep = right ? -3 : 3;
     L.sstep = right ? -1 : 1;
     L.astep = 1;
+    L.m = M;
     return L;
 }
 
@@ -1253,12 +1309,12 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
 
 template <int M>
 __device__ __forceinline__ void stage_row_w(In<M>& sm, int t, int q, double v) {
-    sm.W[q * PSTRIDE + t] = v;
+    sm.W[w_at<M>(q, t)] = v;
     if (!finite(v)) atomicOr(&sm.bad[t], 1);
 }
 template <int M>
 __device__ __forceinline__ void stage_row_t(In<M>& sm, int t, int q, double v) {
-    sm.R[q * PSTRIDE + t] = fast_rcp(v);
+    sm.R[r_at<M>(q, t)] = fast_rcp(v);
     if (!finite_pos(v)) atomicOr(&sm.bad[t], 1);
 }
 
@@ -1278,8 +1334,8 @@ __device__ __forceinline__ void stage_check_ed(In<M>& sm, int t, bool right, con
 template <int M>
 __device__ __forceinline__ void sanitize(In<M>& sm, int lane) {
     if (lane < TPW && sm.bad[lane]) {
-        for (int q = 0; q < (M + 1) * 3; ++q) sm.W[q * PSTRIDE + lane] = 0.0;
-        for (int q = 0; q < M; ++q) sm.R[q * PSTRIDE + lane] = 1.0;
+        for (int q = 0; q < (M + 1) * 3; ++q) sm.W[w_at<M>(q, lane)] = 0.0;
+        for (int q = 0; q < M; ++q) sm.R[r_at<M>(q, lane)] = 1.0;
     }
 }
 
@@ -1691,7 +1747,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
                 dtau = fmin(fmax(dtau, -0.5), 0.5);
                 const double tn = ok ? tl * exp(dtau) : tl;
                 Tl[e] = tn;
-                sm.in.R[phys * PSTRIDE + slot] = fast_rcp(tn);
+                sm.in.R[r_at<M>(phys, slot)] = fast_rcp(tn);
             }
         }
         __syncthreads();
