@@ -102,8 +102,12 @@ constexpr int OSTRIDE = 10;
 // the rows of the second half of the trajectory (knot k with 2k > M, segment i with
 // 2i + 1 > M) hold trajectory t at column t ^ 16, so in every read the pair's two lanes
 // land in opposite bank halves (the middle knot / segment both read is one address).
+// Measured (round 5, profiles/r05_c5_swizzle_ab.jsonl): the conflict cycles of the one-wave
+// class halve (4.23 M -> 2.15 M per call) but its time does not move (0.213-0.216 ms both
+// ways; the whole call 0.481-0.488 vs 0.482-0.493 ms; for every M, where the two-wave
+// class spills 2 VGPRs, 0.480-0.490), so it is off.
 #ifndef TGMS_PAIR_SWIZZLE
-#define TGMS_PAIR_SWIZZLE 1
+#define TGMS_PAIR_SWIZZLE 0
 #endif
 #ifndef TGMS_PAIR_SWIZZLE_MIN_M
 #define TGMS_PAIR_SWIZZLE_MIN_M (TGMS_TWO_WAVE_MAX_M + 1)
