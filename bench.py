@@ -644,16 +644,25 @@ def resolve_topology(gpus: int, env: dict, visible: int):
 
 
 class Lane:
-    """One device's share of the headline: its handle, its `sets` batches, its launch
-    stream (the device's current torch stream) and the captured graph of K steps."""
+    """One device's share of the headline: its handles, its `sets` batches, its launch
+    stream (the device's current torch stream) and the captured graph of K steps.
 
-    def __init__(self, dev: int, gpu_index: int, B: int, M: int, sets: int, method: int):
+    With `streams` > 1 the graph forks: consecutive steps (independent batches) alternate
+    between that many streams, one handle each, joined at the end, so a step's input loads
+    and factorisation run while the previous step's stores drain instead of after its
+    kernel has ended.  Step k uses batch k % sets on stream
+    k % streams: concurrent steps never share a batch, and the steps that do share one run
+    in order on one stream."""
+
+    def __init__(self, dev: int, gpu_index: int, B: int, M: int, sets: int, method: int, streams: int = 1):
         import torch
         from trajectory_generator_ros2_amd import synthetic as S
         from trajectory_generator_ros2_amd.solver import Solver
-        self.dev, self.B, self.M = dev, B, M
+        assert streams >= 1 and sets % streams == 0, "sets must be a multiple of streams"
+        self.dev, self.B, self.M, self.nstreams = dev, B, M, streams
         with torch.cuda.device(dev):
-            self.solver = Solver(dev, method)
+            self.solvers = [Solver(dev, method) for _ in range(streams)]
+            self.solver = self.solvers[0]
             self.bufs = []
             for i in range(sets):
                 _, Wi, Ti = S.uniform_batch(B, M, seed=S.SEED + gpu_index + 7919 * i)
@@ -678,18 +687,27 @@ class Lane:
             raise RuntimeError(f"tgms_solve_uniform_device on device {self.dev}: status {st}: "
                                f"{self.solver.last_error()}")
 
-    def capture(self, K: int):
+    def capture(self, K: int, streams: int = 0):
         """The K steps captured once into a HIP graph (thread-local capture: another
-        thread -- the RCCL watchdog at N > 1 ranks -- may keep making HIP calls)."""
+        thread -- the RCCL watchdog at N > 1 ranks -- may keep making HIP calls); `streams`
+        (default: the lane's) launch streams, forked from and joined to the capture stream."""
         import torch
+        n = streams or self.nstreams
         with torch.cuda.device(self.dev):
             cap = torch.cuda.Stream(device=self.dev)
+            side = [torch.cuda.Stream(device=self.dev) for _ in range(n - 1)]
             cap.wait_stream(self.stream)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=cap, capture_error_mode="thread_local"):
+                for s in side:
+                    s.wait_stream(cap)
                 for k in range(K):
                     dWk, dTk, dCk, dSk = self.bufs[k % len(self.bufs)]
-                    self.solver.solve_uniform_device(self.B, self.M, dWk, dTk, dCk, dSk, stream=cap.cuda_stream)
+                    i = k % n
+                    st = cap if i == 0 else side[i - 1]
+                    self.solvers[i].solve_uniform_device(self.B, self.M, dWk, dTk, dCk, dSk, stream=st.cuda_stream)
+                for s in side:
+                    cap.wait_stream(s)
             self.stream.wait_stream(cap)
             g.replay()  # warm replay (graph upload)
             torch.cuda.synchronize(self.dev)
@@ -868,6 +886,11 @@ def main():
     ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the K timed steps replayed from one captured HIP graph; 0: K Python-level launches")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launch streams per device in the captured graph: consecutive steps (independent "
+                         "batches) alternate between them, one handle each, so a step's loads and "
+                         "factorisation overlap the previous step's store drain; 1: steps back to back. The "
+                         "roofline is timed separately with one stream (kernel durations, as rocprofv3 sees them)")
     ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
     ap.add_argument("--band-steps", type=int, default=5, help="steps of the band-KKT side line (0: skip)")
     ap.add_argument("--sample-traj", type=int, default=4096,
@@ -924,7 +947,10 @@ def main():
     method = METHOD_DENSE_KKT if args.method == "dense" else METHOD_REDUCED
     # this process's devices, each with its own shard of the job: `sets` independent
     # batches of independent trajectories (set 0: seed + GPU index, as every side line uses)
-    lanes = [Lane(d, rank if mode == "ranks" else d, B, M, sets, method) for d in devs]
+    nstreams = max(1, args.streams) if args.graph else 1
+    if sets % nstreams:
+        raise SystemExit(f"bench.py: --sets {sets} must be a multiple of --streams {nstreams}")
+    lanes = [Lane(d, rank if mode == "ranks" else d, B, M, sets, method, nstreams) for d in devs]
     torch.cuda.set_device(devs[0])
     lane0 = lanes[0]
     solver, dev, stream = lane0.solver, lane0.dev, lane0.stream
@@ -950,6 +976,9 @@ def main():
     for L in lanes:
         for k in range(max(args.warmup, sets)):
             L.step(k)
+        for sv in L.solvers[1:]:  # the other streams' handles: first calls outside any capture
+            b = L.bufs[0]
+            sv.solve_uniform_device(B, M, b[0], b[1], b[2], b[3], stream=L.stream.cuda_stream)
     sync_all()
     assert all(L.failures() == 0 for L in lanes), "solver reported failures"
 
@@ -993,12 +1022,36 @@ def main():
     barrier()
     el = all_ranks(time.perf_counter() - t0, dist.ReduceOp.MAX if world > 1 else None)
     launch_each = [L.ev0.elapsed_time(L.ev1) / K for L in lanes]
-    launch_ms_max = all_ranks(max(launch_each), dist.ReduceOp.MAX if world > 1 else None)
-    launch_ms_min = all_ranks(min(launch_each), dist.ReduceOp.MIN if world > 1 else None)
+    step_ms_max = all_ranks(max(launch_each), dist.ReduceOp.MAX if world > 1 else None)
     assert all(L.failures() == 0 for L in lanes), "solver reported failures"
-    launch_mode = "hip_graph_of_K_steps" if graphed else "python_loop"
+    launch_mode = ("hip_graph_of_K_steps" + (f"_over_{nstreams}_streams" if nstreams > 1 else "")) if graphed \
+        else "python_loop"
     for L in lanes:
         L.graph = None
+    # The roofline is the kernel's own rate: with steps overlapping across streams a step's
+    # share of the timed region is shorter than a kernel's duration, so the K steps are
+    # timed again back to back on one stream (the same kernels rocprofv3 reports, their
+    # durations adding up to the region).
+    if graphed and nstreams > 1:
+        for L in lanes:
+            L.capture(K, streams=1)
+        barrier()
+        sync_all()
+        for L in lanes:
+            L.ev0.record(L.stream)
+            with torch.cuda.device(L.dev):
+                L.graph.replay()
+            L.ev1.record(L.stream)
+        sync_all()
+        barrier()
+        kernel_each = [L.ev0.elapsed_time(L.ev1) / K for L in lanes]
+        assert all(L.failures() == 0 for L in lanes), "solver reported failures"
+        for L in lanes:
+            L.graph = None
+    else:
+        kernel_each = launch_each
+    launch_ms_max = all_ranks(max(kernel_each), dist.ReduceOp.MAX if world > 1 else None)
+    launch_ms_min = all_ranks(min(kernel_each), dist.ReduceOp.MIN if world > 1 else None)
 
     per_launch = launch_stats(solver, B, M, lane0.bufs, stream)
     cache_res = None
@@ -1133,7 +1186,8 @@ def main():
                                    f"coefficients [traj][seg][axis][8] fp64 in HBM; a fresh batch every step "
                                    f"({sets} batches rotated, {sets * bpl / 1e6:.0f} MB per GPU)",
                        "batch_per_gpu": B, "segments": M, "sets": sets, "method": args.method,
-                       "launch": launch_mode, "processes": world, "devices_per_process": len(devs),
+                       "launch": launch_mode, "streams_per_device": nstreams,
+                       "processes": world, "devices_per_process": len(devs),
                        "parallelism": parallelism},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -1153,7 +1207,14 @@ def main():
                          "floor_source": "profiles/archive/r03_runstore_occ.txt (reads + stores, no compute, 2 waves/SIMD, "
                                          "4 rounds: 28.6 us for 22.5 MB read + 126 MB written)",
                          "launch_ms_rank_min": launch_ms_min, "launch_ms_rank_max": launch_ms_max,
-                         "algorithmic_bytes_per_launch": bpl},
+                         "launch_ms_how": ("the K steps back to back on one stream, timed after the headline "
+                                           "region (kernel durations)" if nstreams > 1 and graphed else
+                                           "the headline region's events / K"),
+                         "algorithmic_bytes_per_launch": bpl,
+                         # the headline region itself: steps overlapping across the streams
+                         "pipelined": {"streams": nstreams, "ms_per_step_events": step_ms_max,
+                                       "achieved": bpl / (step_ms_max * 1e-3) / 1e9,
+                                       "frac": bpl / (step_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS}},
             "cpu_baseline": cpu,
             "per_launch": per_launch,
             "cache_resident": cache_res,
@@ -1174,7 +1235,8 @@ def main():
         print(json.dumps(line), flush=True)
     barrier()
     for L in lanes:
-        L.solver.close()
+        for sv in L.solvers:
+            sv.close()
     if world > 1:
         dist.destroy_process_group()
 
