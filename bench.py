@@ -886,7 +886,7 @@ def main():
     ap.add_argument("--method", choices=["reduced", "dense"], default="reduced")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the K timed steps replayed from one captured HIP graph; 0: K Python-level launches")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="launch streams per device in the captured graph: consecutive steps (independent "
                          "batches) alternate between them, one handle each, so a step's loads and "
                          "factorisation overlap the previous step's store drain; 1: steps back to back. The "
