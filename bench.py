@@ -913,6 +913,9 @@ def main():
     ap.add_argument("--full-lines-timeout", type=float, default=300.0,
                     help="seconds the N > 1 library multi-GPU side lines may take before they are abandoned")
     args = ap.parse_args()
+    # concurrent steps must never share a batch: step k runs batch k % sets on stream k % streams
+    if args.graph and args.streams > 1 and max(1, args.sets) % args.streams:
+        raise SystemExit(f"bench.py: --sets {args.sets} must be a multiple of --streams {args.streams}")
 
     import torch
     import torch.distributed as dist
@@ -948,8 +951,6 @@ def main():
     # this process's devices, each with its own shard of the job: `sets` independent
     # batches of independent trajectories (set 0: seed + GPU index, as every side line uses)
     nstreams = max(1, args.streams) if args.graph else 1
-    if sets % nstreams:
-        raise SystemExit(f"bench.py: --sets {sets} must be a multiple of --streams {nstreams}")
     lanes = [Lane(d, rank if mode == "ranks" else d, B, M, sets, method, nstreams) for d in devs]
     torch.cuda.set_device(devs[0])
     lane0 = lanes[0]

@@ -36,3 +36,15 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode != 0
     assert "--gpus 2 but only" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_bench_refuses_streams_that_would_share_a_batch():
+    """With --streams S the timed steps alternate over S streams and step k solves batch
+    k % sets: unless S divides sets, two steps in flight at once could write one batch.
+    bench.py refuses before touching a GPU."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--streams", "3", "--sets", "4",
+                        "--steps", "1"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "must be a multiple of --streams 3" in r.stderr
+    assert r.stdout.strip() == ""
