@@ -129,12 +129,17 @@ def _timed_reps(fn, n_per_call: int, target_s: float):
     return n_per_call * reps / el, reps, el
 
 
-def cpu_baseline(B: int, M: int, target_s: float):
+def cpu_baseline(B: int, M: int, target_s: float, check=None):
     """CPU restatement of the solve (the reference has no solver to time, SURVEY.md §0,
     §8(d)): the oracle's fp64 C code with OpenMP over trajectories, on every core this
     process may use, on a bounded sample of the same workload.  `value` is its reduced
     formulation (the GPU kernel's math, O(M) per trajectory: the strongest CPU
-    restatement); the survey's literal dense-KKT LU and the one-core rates are beside it."""
+    restatement); the survey's literal dense-KKT LU and the one-core rates are beside it.
+
+    The timed sample is rank 0's batch 0 (seed 20251015), the batch the headline's steps
+    k = 0 mod sets solved: `check` ([B', 3, 8], what the timed region wrote for its first B'
+    trajectories) is compared with the baseline's own last output, norm-wise per
+    (trajectory, axis), outside every timed region.  Returns (line, check result)."""
     from oracle import oracle as O
     from trajectory_generator_ros2_amd import synthetic as S
     O.build()
@@ -142,9 +147,10 @@ def cpu_baseline(B: int, M: int, target_s: float):
     threads = cores["usable"]
     so, W, T = S.uniform_batch(B, M)
     W, T = W.reshape(-1, 3), T.reshape(-1)
+    last = {}
 
     def reduced():
-        _, st = O.solve_batch(so, W, T, None, O.REDUCED, threads)
+        last["C"], st = O.solve_batch(so, W, T, None, O.REDUCED, threads)
         assert (st == 0).all()
 
     red_rate, red_reps, red_s = _timed_reps(reduced, B, 0.6 * target_s)
@@ -163,13 +169,22 @@ def cpu_baseline(B: int, M: int, target_s: float):
     t1 = time.perf_counter()
     O.solve_batch(so[:1025], W[: 1024 * (M + 1)], T[: 1024 * M], None, O.KKT_C4, 1)
     dense_1 = 1024 / (time.perf_counter() - t1)
+    res = None
+    if check is not None:
+        n = check.shape[0] // M
+        R = last["C"][: n * M].reshape(n, M, 3, 8)
+        G = check.reshape(n, M, 3, 8)
+        den = np.abs(R).max(axis=(1, 3))
+        err = np.abs(G - R).max(axis=(1, 3)) / np.where(den == 0.0, 1.0, den)
+        res = {"trajectories": n, "max_rel_err": float(err.max()), "tol": 1e-9,
+               "ok": bool(np.isfinite(G).all() and err.max() <= 1e-9)}
     return {"value": red_rate, "unit": "trajectories/s", "cores": threads, "kind": "cpu_restatement",
             "what": "cpu_restatement (reference has no solver): oracle/minsnap_oracle.c, fp64, OpenMP",
             "cores_detail": cores, "cpu_model": _cpu_model(),
             "value_1core": red_1, "dense_kkt_value": dense_rate, "dense_kkt_value_1core": dense_1,
             "sample": f"reduced formulation: {red_reps} x {B} trajectories of the config-3 workload (M={M}), "
                       f"{red_s:.1f} s; dense KKT (LU, partial pivoting): {dense_reps} x {n}, {dense_s:.1f} s; "
-                      f"{threads} OpenMP thread(s)"}
+                      f"{threads} OpenMP thread(s)"}, res
 
 
 C5_PMC_FILE = "profiles/c5_pmc.json"
@@ -716,6 +731,37 @@ class Lane:
     def failures(self) -> int:
         return sum(int((b[3] != 0).sum().item()) for b in self.bufs)
 
+    def reset_outputs(self):
+        """Every set's coefficients to NaN and statuses to -1 (no solve writes -1), so a
+        check after a timed region sees only what that region wrote."""
+        import torch
+        with torch.cuda.device(self.dev):
+            for b in self.bufs:
+                b[2].fill_(float("nan"))
+                b[3].fill_(-1)
+            torch.cuda.synchronize(self.dev)
+
+    def verify(self, K: int) -> dict:
+        """After a timed region of K steps: every set a step wrote (set k % sets for k < K)
+        has status 0 everywhere and coefficients bit-identical to a fresh one-stream solve
+        of the same batch by this lane's first handle (outside any graph)."""
+        import torch
+        stepped = sorted({k % len(self.bufs) for k in range(K)})
+        status_ok, equal = True, True
+        with torch.cuda.device(self.dev):
+            ref = torch.empty_like(self.bufs[0][2])
+            rst = torch.empty_like(self.bufs[0][3])
+            for i in stepped:
+                dW, dT, dC, dS = self.bufs[i]
+                status_ok &= bool((dS == 0).all().item())
+                ref.fill_(float("nan"))
+                rst.fill_(-1)
+                self.solver.solve_uniform_device(self.B, self.M, dW, dT, ref, rst, stream=self.stream.cuda_stream)
+                torch.cuda.synchronize(self.dev)
+                equal &= bool(torch.equal(ref, dC)) and bool((rst == 0).all().item())
+        return {"sets_checked": len(stepped), "sets": len(self.bufs), "status_ok": status_ok,
+                "bitwise_equal_one_stream_resolve": equal}
+
 
 def _timed_multi(fn, dev0_stream, reps: int, devs):
     """Run fn() `reps` times after one warm call; wall clock between synchronisations of
@@ -1007,6 +1053,9 @@ def main():
             for L in lanes:
                 L.graph = None  # some rank could not capture: every rank times the launch loop
     graphed = all(L.graph is not None for L in lanes)
+    # the timed region must prove its own output: every set back to NaN / status -1 first
+    for L in lanes:
+        L.reset_outputs()
     barrier()
     sync_all()
     t0 = time.perf_counter()
@@ -1024,7 +1073,12 @@ def main():
     el = all_ranks(time.perf_counter() - t0, dist.ReduceOp.MAX if world > 1 else None)
     launch_each = [L.ev0.elapsed_time(L.ev1) / K for L in lanes]
     step_ms_max = all_ranks(max(launch_each), dist.ReduceOp.MAX if world > 1 else None)
-    assert all(L.failures() == 0 for L in lanes), "solver reported failures"
+    # outside the timed region: what the K steps wrote, against a one-stream re-solve
+    checks = [L.verify(K) for L in lanes]
+    ver_ok = all(c["status_ok"] and c["bitwise_equal_one_stream_resolve"] for c in checks)
+    ver_ok = all_ranks(1.0 if ver_ok else 0.0, dist.ReduceOp.MIN if world > 1 else None) == 1.0
+    assert ver_ok, f"the timed region's output failed verification: {checks}"
+    timed_set0 = lane0.bufs[0][2][: min(B, 65536)].cpu().numpy().reshape(-1, 3, 8) if rank == 0 else None
     launch_mode = ("hip_graph_of_K_steps" + (f"_over_{nstreams}_streams" if nstreams > 1 else "")) if graphed \
         else "python_loop"
     for L in lanes:
@@ -1155,8 +1209,9 @@ def main():
     # rank-0-only host work, after every GPU timing (the other ranks wait at the
     # final barrier)
     cpu = None
+    oracle_check = {"skipped": "--cpu-seconds 0 (the check is the CPU baseline's own output)"}
     if rank == 0 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(B, M, args.cpu_seconds)
+        cpu, oracle_check = cpu_baseline(B, M, args.cpu_seconds, check=timed_set0)
 
     if rank == 0:
         bpl = algorithmic_bytes_per_traj(M) * B
@@ -1185,7 +1240,8 @@ def main():
                     "waypoints, T=clip(|dw|/1m/s,0.5,10), rest-to-rest)",
             "config": {"workload": f"config3: {B} trajectories/GPU x {M} segments, order 7, 3 axes, "
                                    f"coefficients [traj][seg][axis][8] fp64 in HBM; a fresh batch every step "
-                                   f"({sets} batches rotated, {sets * bpl / 1e6:.0f} MB per GPU)",
+                                   f"({sets} batches rotated, {sets * bpl / 1e6:.0f} MB per GPU), "
+                                   f"{nstreams} launch stream(s) per device",
                        "batch_per_gpu": B, "segments": M, "sets": sets, "method": args.method,
                        "launch": launch_mode, "streams_per_device": nstreams,
                        "processes": world, "devices_per_process": len(devs),
@@ -1216,6 +1272,13 @@ def main():
                          "pipelined": {"streams": nstreams, "ms_per_step_events": step_ms_max,
                                        "achieved": bpl / (step_ms_max * 1e-3) / 1e9,
                                        "frac": bpl / (step_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+            # the timed region's own output: every set reset to NaN /
+            # status -1 before it, then bit-compared with a one-stream re-solve and (set 0,
+            # rank 0) with the CPU baseline's oracle output
+            "verified": bool(ver_ok and (oracle_check.get("ok", True))),
+            "verification": {"per_device": checks, "oracle": oracle_check},
+            # the same K steps back to back on one stream (rounds 1-4's headline form)
+            "value_one_stream": n_total * B / (launch_ms_max * 1e-3),
             "cpu_baseline": cpu,
             "per_launch": per_launch,
             "cache_resident": cache_res,

@@ -76,7 +76,10 @@ typedef enum tgms_status {
     TGMS_ERR_NONFINITE = 3,   /* solution contains inf/nan */
     TGMS_ERR_NO_DEVICE = 4,   /* no HIP device (no CPU fallback exists) */
     TGMS_ERR_DEVICE = 5,      /* a HIP runtime call failed (see tgms_last_error) */
-    TGMS_ERR_UNSUPPORTED = 6  /* e.g. dense-KKT method with M_b > TGMS_DENSE_MAX_SEGMENTS */
+    TGMS_ERR_UNSUPPORTED = 6, /* e.g. dense-KKT method with M_b > TGMS_DENSE_MAX_SEGMENTS */
+    TGMS_ERR_SKIPPED = 7      /* per trajectory only: not solved because another trajectory of
+                                 the same device shard piece had invalid offsets
+                                 (tgms_refine_loop_multi_device; that one is INVALID_ARG) */
 } tgms_status;
 
 typedef enum tgms_method {
@@ -134,8 +137,12 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M,
  * detection); tgms_refine_loop_multi_device reads only seg_offsets[0], [B] and the shard
  * and piece cuts (binary search), so per-trajectory M is checked on the devices alone.
  * Device offsets with an M outside 1..16 or another span run nothing in the shard piece
- * that holds them and mark its trajectories TGMS_ERR_INVALID_ARG in d_status, with zero
- * coefficients and costs and the times kept; the call itself returns TGMS_OK. */
+ * that holds them (failure granularity: one piece of one device's shard, <= 1/4 of the
+ * shard): in d_status the trajectories whose own M is outside 1..16 read
+ * TGMS_ERR_INVALID_ARG and the piece's other trajectories TGMS_ERR_SKIPPED, all with zero
+ * coefficients and costs and the times kept; the call itself returns TGMS_OK, so a caller
+ * checks d_status (a device-side finding cannot reach the return code without a
+ * synchronisation the pipelined call avoids). */
 tgms_status tgms_solve_batch_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
                                     const int32_t* d_seg_offsets, const double* d_waypoints,
                                     const double* d_seg_times, const double* d_end_derivs,

@@ -14,6 +14,17 @@ with no rounding at all.  Two formulations are provided:
                        (v, a, j at interior knots), using the exactly derived
                        septic-Hermite snap-cost matrix.
 
+For the time-allocation refinement:
+
+* ``refine_grad``    – the exact per-segment snap cost J_i and its derivative
+                       dJ_i/dT_i at the optimal knot data (envelope theorem), from
+                       the definition sum_ab KH_ab T^(s_a+s_b-7) g_a g_b — no
+                       displacement form, no rounding;
+* ``optimal_cost``   – the exact optimal cost J*(T) = sum_i J_i, so a test can
+                       check dJ_i/dT_i against an exact central difference of J*;
+* ``refine_step``    – one step T_1 = T_0 exp(clamp(-eta T_0 (dJ + k_T) / F, +-1/2))
+                       with F exact and exp in mpmath at 40 digits, rounded once.
+
 For M <= 4 the tests require both to return *identical rationals*, which proves
 the reduced formulation (the one the HIP kernel uses) is the same problem as the
 KKT the north star names; the reduced solver then produces exact goldens up to
@@ -142,7 +153,11 @@ def kkt_solve(waypoints, seg_times, end_derivs=None, cont: int = 4):
 
 def reduced_solve(waypoints, seg_times, end_derivs=None):
     """Exact solve through the reduced Hessian over free knot derivatives."""
-    M, W, T, ED = _as_frac_traj(waypoints, seg_times, end_derivs)
+    return _reduced(*_as_frac_traj(waypoints, seg_times, end_derivs))[0]
+
+
+def _reduced(M, W, T, ED):
+    """Exact reduced solve: (coeffs[M][3][8], knot data kd(knot, axis) -> [p, v, a, j])."""
     nf = 3 * (M - 1)
 
     def known(knot, d, a):
@@ -188,7 +203,70 @@ def reduced_solve(waypoints, seg_times, end_derivs=None):
             d = [sum(_E[j][q] * h[q] for q in range(8)) for j in range(8)]
             seg.append([d[j] / T[i] ** j for j in range(8)])
         C.append(seg)
-    return C
+    return C, kd
+
+
+def _segment_cost(T: F, g0, g1):
+    """J and dJ/dT of one axis of one segment from its end data, by definition."""
+    g = list(g0) + list(g1)
+    j = dj = F(0)
+    for x in range(8):
+        for y in range(8):
+            n = _SIG[x] + _SIG[y] - 7
+            k = _KH[x][y] * g[x] * g[y]
+            j += k * T ** n
+            dj += k * n * T ** (n - 1)
+    return j, dj
+
+
+def refine_grad(waypoints, seg_times, end_derivs=None):
+    """Exact per-segment snap cost J_i and dJ_i/dT_i (knot data held at the optimum)."""
+    M, W, T, ED = _as_frac_traj(waypoints, seg_times, end_derivs)
+    _, kd = _reduced(M, W, T, ED)
+    J, dJ = [], []
+    for i in range(M):
+        ji = dji = F(0)
+        for a in range(3):
+            j, dj = _segment_cost(T[i], kd(i, a), kd(i + 1, a))
+            ji += j
+            dji += dj
+        J.append(ji)
+        dJ.append(dji)
+    return J, dJ
+
+
+def optimal_cost(waypoints, seg_times, end_derivs=None):
+    """Exact optimal snap cost J*(T) for times given as Fractions or floats."""
+    M = len(seg_times)
+    W = [[F(float(waypoints[i][a])) for a in range(3)] for i in range(M + 1)]
+    T = [t if isinstance(t, F) else F(float(t)) for t in seg_times]
+    if end_derivs is None:
+        ED = [[[F(0)] * 3 for _ in range(3)] for _ in range(2)]
+    else:
+        ED = [[[F(float(end_derivs[e][k][a])) for a in range(3)] for k in range(3)] for e in range(2)]
+    _, kd = _reduced(M, W, T, ED)
+    return sum(_segment_cost(T[i], kd(i, a), kd(i + 1, a))[0] for i in range(M) for a in range(3))
+
+
+def refine_step(seg_times, J, dJ, k_T: float, eta: float):
+    """One refinement step from exact J_i, dJ_i: returns (F, T_1 as floats).
+
+    F = sum J_i + k_T sum T_i (exact), dtau_i = clamp(-eta T_i (dJ_i + k_T) / F, -1/2, 1/2)
+    (exact), T_1 = T_i exp(dtau_i) in mpmath at 40 significant digits, rounded to fp64 once.
+    The step is csrc/tgms_reduced.hip's and oracle_refine_times' (SURVEY.md §8(f) rank 2)."""
+    import mpmath
+    T = [F(float(t)) for t in seg_times]
+    kT, et = F(float(k_T)), F(float(eta))
+    Fv = sum(J) + kT * sum(T)
+    half = F(1, 2)
+    out = []
+    with mpmath.workdps(40):
+        for Ti, g in zip(T, dJ):
+            d = -et * Ti * (g + kT) / Fv
+            d = min(max(d, -half), half)
+            x = mpmath.mpf(Ti.numerator) / Ti.denominator * mpmath.exp(mpmath.mpf(d.numerator) / d.denominator)
+            out.append(float(x))
+    return Fv, out
 
 
 def eval_exact(coeffs_seg_axis: Sequence[F], t: F, k: int) -> F:

@@ -60,19 +60,6 @@ static int inputs_valid(int M, const double* W, const double* T, const double* E
 }
 
 /* end derivative k (1..3) at end e (0 start, 1 final), axis a */
-/* Value and first three derivatives of one axis' monomial coefficients at t. */
-static void eval_poly_at(const double* c, double t, double out[4]) {
-    for (int k = 0; k < 4; ++k) {
-        double s = 0.0;
-        for (int j = 7; j >= k; --j) {
-            double f = 1.0;
-            for (int q = 0; q < k; ++q) f *= (double)(j - q);
-            s = s * t + f * c[j];
-        }
-        out[k] = s;
-    }
-}
-
 static double end_deriv(const double* ED, int e, int k, int a) {
     return ED ? ED[e * 9 + (k - 1) * 3 + a] : 0.0;
 }
@@ -480,24 +467,39 @@ int oracle_solve_batch(int formulation, int32_t B, const int32_t* seg_offsets,
  * end data g = (w0, v0, a0, j0, w1, v1, a1, j1) per axis (KH above):
  *   J = sum_ab KH[a][b] T^(s_a+s_b-7) g_a g_b,
  *   dJ/dT = sum_ab KH[a][b] (s_a+s_b-7) T^(s_a+s_b-8) g_a g_b
- * (knot data held fixed: at the optimum only the explicit T dependence counts). */
-static void segment_cost(const double* c, const double* w0, const double* w1, double T, double* J, double* dJ) {
+ * (knot data held fixed: at the optimum only the explicit T dependence counts).
+ * Evaluated in displacement form, as solve_reduced forms its right-hand side: with the
+ * scaled data h_a = T^s_a g_a, J = T^-7 h^T KH h and dJ/dT = T^-8 h^T (KH o (s_a+s_b-7)) h;
+ * KH (and its weighted copy, s = 0 at both positions) annihilates a common shift of the
+ * two positions, so h_0 = 0 and h_4 = w1 - w0 — no absolute positions against KH's
+ * +-100,800 entries.  The knot data are the solve's own: the start (v, a, j) are segment
+ * i's c1, 2 c2, 6 c3; the end data are segment i+1's start (the shared knot) or the end
+ * derivatives — no re-evaluation of the septic at T (whose terms cancel), no pow(). */
+static void segment_cost(const double* c, const double* cn, const double* ED, const double* w0,
+                         const double* w1, double T, double* J, double* dJ) {
+    const double T2 = T * T, T3 = T2 * T, T4 = T2 * T2;
+    const double T7 = T4 * T3, T8 = T4 * T4;
     double j = 0.0, dj = 0.0;
     for (int a = 0; a < 3; ++a) {
         const double* ca = c + 8 * a;
-        double e1[4];
-        eval_poly_at(ca, T, e1);
-        const double g[8] = {w0[a], ca[1], 2.0 * ca[2], 6.0 * ca[3], w1[a], e1[1], e1[2], e1[3]};
-        for (int x = 0; x < 8; ++x)
+        double e1[3];
+        for (int d = 1; d <= 3; ++d)
+            e1[d - 1] = cn ? (d == 1 ? cn[8 * a + 1] : d == 2 ? 2.0 * cn[8 * a + 2] : 6.0 * cn[8 * a + 3])
+                           : end_deriv(ED, 1, d, a);
+        const double h[8] = {0.0, ca[1] * T, 2.0 * ca[2] * T2, 6.0 * ca[3] * T3,
+                             w1[a] - w0[a], e1[0] * T, e1[1] * T2, e1[2] * T3};
+        for (int x = 0; x < 8; ++x) {
+            double sj = 0.0, sd = 0.0;
             for (int y = 0; y < 8; ++y) {
-                const int n = SIG[x] + SIG[y] - 7;
-                const double k = KH[x][y] * g[x] * g[y];
-                j += k * pow(T, n);
-                dj += k * n * pow(T, n - 1);
+                sj += KH[x][y] * h[y];
+                sd += KH[x][y] * (double)(SIG[x] + SIG[y] - 7) * h[y];
             }
+            j += h[x] * sj;
+            dj += h[x] * sd;
+        }
     }
-    *J = j;
-    *dJ = dj;
+    *J = j / T7;
+    *dJ = dj / T8;
 }
 
 int oracle_refine_times(int formulation, int M, const double* W, double* T, const double* ED, double kT,
@@ -510,7 +512,8 @@ int oracle_refine_times(int formulation, int M, const double* W, double* T, cons
         if (st != ORACLE_OK) return st;
         double Jv[ORACLE_MAX_SEGMENTS], dJv[ORACLE_MAX_SEGMENTS], F = 0.0;
         for (int i = 0; i < M; ++i) {
-            segment_cost(c + 24 * i, W + 3 * i, W + 3 * (i + 1), T[i], &Jv[i], &dJv[i]);
+            segment_cost(c + 24 * i, i + 1 < M ? c + 24 * (i + 1) : NULL, ED, W + 3 * i, W + 3 * (i + 1), T[i],
+                         &Jv[i], &dJv[i]);
             F += Jv[i] + kT * T[i];
         }
         if (it == iters) { /* final times: report F, keep the final solve in C */
@@ -539,7 +542,8 @@ int oracle_refine_grad(int formulation, int M, const double* W, const double* T,
     double F = 0.0;
     for (int i = 0; i < M; ++i) {
         double J;
-        segment_cost(c + 24 * i, W + 3 * i, W + 3 * (i + 1), T[i], &J, &dJ[i]);
+        segment_cost(c + 24 * i, i + 1 < M ? c + 24 * (i + 1) : NULL, ED, W + 3 * i, W + 3 * (i + 1), T[i], &J,
+                     &dJ[i]);
         F += J + kT * T[i];
     }
     if (cost) *cost = F;

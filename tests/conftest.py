@@ -165,3 +165,45 @@ def check_spline_properties_chunked(so, W, T, C, chunk=65536, **kw):
         hi = min(B, lo + chunk)
         s0, s1 = int(so[lo]), int(so[hi])
         check_spline_properties(so[lo:hi + 1] - s0, W[s0 + lo:s1 + hi + 1], T[s0:s1], C[s0:s1], **kw)
+
+
+REFINE_GROUPS = ("u10", "u10e", "u7e", "u16", "r", "re", "u257", "u257e", "r257", "r257e")
+
+
+def load_refine_golden():
+    """tests/golden/refine_grad.npz (exact config-5 step, make_golden.py): returns
+    (k_T, eta, {group: dict(seg_offsets, waypoints, seg_times, end_derivs|None, J, dJ, F, T1)})."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "refine_grad.npz"))
+    groups = {}
+    for g in REFINE_GROUPS:
+        d = {k: z[g + "_" + k] for k in ("seg_offsets", "waypoints", "seg_times", "J", "dJ", "F", "T1")}
+        d["end_derivs"] = z[g + "_end_derivs"] if (g + "_end_derivs") in z.files else None
+        groups[g] = d
+    return float(z["k_T"]), float(z["eta"]), groups
+
+
+def recovered_gradient(T0, T1, F0, k_T, eta):
+    """The per-segment dJ_i/dT_i a refinement step applied, recovered from its output:
+    T1 = T0 exp(-eta T0 (dJ + k_T) / F0)  =>  dJ = -log(T1/T0) F0 / (eta T0) - k_T.
+    Also returns the mask of unclamped segments (|dtau| < 1/2)."""
+    dtau = np.log(np.asarray(T1) / np.asarray(T0))
+    return -dtau * F0 / (eta * T0) - k_T, np.abs(dtau) < 0.499
+
+
+def gradient_rel_err(so, g, ref, mask=None):
+    """Worst per-trajectory norm-wise error max_i |g_i - ref_i| / max_i |ref_i| over a CSR
+    batch (segments outside `mask` are skipped in the numerator)."""
+    so = np.asarray(so, dtype=np.int64)
+    d = np.abs(np.asarray(g) - np.asarray(ref))
+    if mask is not None:
+        d = np.where(mask, d, 0.0)
+    num = np.maximum.reduceat(d, so[:-1])
+    den = np.maximum.reduceat(np.abs(ref), so[:-1])
+    return float((num / np.where(den == 0.0, 1.0, den)).max())
+
+
+def solve_goldens():
+    """The solve fixtures of tests/golden (every *.npz except the refinement step's)."""
+    import glob
+    return sorted(p for p in glob.glob(os.path.join(ROOT, "tests", "golden", "*.npz"))
+                  if os.path.basename(p) != "refine_grad.npz")

@@ -12,6 +12,15 @@ exactly and asserts the two rational solutions are identical.
 Outputs (numpy .npz, no pickles): one file per case with
     seg_offsets int32 [B+1], waypoints [S+B,3], seg_times [S], end_derivs [B,18] (optional),
     coeffs [S,3,8] (exact, rounded), and for sampled cases dt, sample_offsets, samples [n,12].
+
+refine_grad.npz (the config-5 step) holds ten groups, each
+prefixed ``<g>_`` (u10, u10e: uniform M = 10 without / with end derivatives; u7e: M = 7
+with; u16: M = 16; r, re: ragged M in 1..16, every M at least twice, without / with;
+u257, u257e, r257, r257e: the 257-trajectory inputs of test_gpu_parity.py's one-step test):
+    seg_offsets, waypoints, seg_times, end_derivs (the "e" groups),
+    J [S], dJ [S]  exact per-segment snap cost and dJ_i/dT_i, rounded once,
+    F [B]          exact F = sum J + k_T sum T, rounded once,
+    T1 [S]         one step at (k_T, eta) = (REFINE_KT, REFINE_ETA): mpmath exp, rounded once.
 """
 from __future__ import annotations
 
@@ -48,6 +57,36 @@ def _solve_all(Ws, Ts, EDs=None, check_kkt_upto=5):
 
 
 ONLY = set(sys.argv[1:])
+REFINE_KT, REFINE_ETA = 1.0, 0.02
+
+
+def _refine_one(args):
+    w, t, ed = args
+    J, dJ = X.refine_grad(w, t, None if ed is None else np.asarray(ed).reshape(2, 3, 3))
+    Fv, T1 = X.refine_step(t, J, dJ, REFINE_KT, REFINE_ETA)
+    return [float(v) for v in J], [float(v) for v in dJ], float(Fv), T1
+
+
+def save_refine(groups):
+    """groups: {name: (Ws, Ts, EDs or None)} -> refine_grad.npz (exact, parallel)."""
+    if ONLY and "refine_grad" not in ONLY:
+        return
+    from multiprocessing import Pool
+    d = dict(k_T=np.float64(REFINE_KT), eta=np.float64(REFINE_ETA))
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        for g, (Ws, Ts, EDs) in groups.items():
+            so, W, T = _csr(Ws, Ts)
+            res = pool.map(_refine_one, [(w, t, None if EDs is None else EDs[i]) for i, (w, t) in
+                                         enumerate(zip(Ws, Ts))])
+            d[g + "_seg_offsets"], d[g + "_waypoints"], d[g + "_seg_times"] = so, W, T
+            if EDs is not None:
+                d[g + "_end_derivs"] = np.asarray(EDs, float).reshape(-1, 18)
+            d[g + "_J"] = np.concatenate([r[0] for r in res])
+            d[g + "_dJ"] = np.concatenate([r[1] for r in res])
+            d[g + "_F"] = np.asarray([r[2] for r in res])
+            d[g + "_T1"] = np.concatenate([r[3] for r in res])
+            print("refine_grad", g, "B=%d S=%d" % (len(Ts), int(so[-1])))
+    np.savez_compressed(os.path.join(HERE, "refine_grad.npz"), **d)
 
 
 def save(name, Ws, Ts, EDs=None, sample_dt=None):
@@ -119,6 +158,35 @@ def main():
         s = np.sort(rng.uniform(-3, 3, 6))
         Wl.append(a + s[:, None] * d); Tl.append(rng.uniform(0.5, 3.0, 5))
     save("collinear", Wl, Tl)
+    # config-5 refinement step: exact gradient and one exact step
+    rr = np.random.default_rng(64)
+    ed = lambda n: list(rr.normal(scale=0.3, size=(n, 18)))
+    groups = {}
+    for g, B, M, with_ed in (("u10", 32, 10, False), ("u10e", 32, 10, True), ("u7e", 16, 7, True),
+                             ("u16", 16, 16, False)):
+        _, Wu, Tu = S.uniform_batch(B, M, seed=3000 + M + 100 * with_ed)
+        groups[g] = (list(Wu), list(Tu), ed(B) if with_ed else None)
+    for g, with_ed in (("r", False), ("re", True)):
+        Ms = list(range(1, 17)) * 2 + list(rr.integers(1, 17, size=8))
+        Wr, Tr = [], []
+        for i, m in enumerate(Ms):
+            _, w, t = S.uniform_batch(1, int(m), seed=4000 + 100 * with_ed + i)
+            Wr.append(w[0]); Tr.append(t[0])
+        groups[g] = (Wr, Tr, ed(len(Ms)) if with_ed else None)
+    # the one-step GPU test's own inputs (tests/test_gpu_parity.py): 257 trajectories each
+    for ragged in (False, True):
+        if ragged:
+            so, W, T = S.ragged_batch(257, 1, 16, seed=61)
+        else:
+            so, W, T = S.uniform_batch(257, 10, seed=62)
+        W, T = W.reshape(-1, 3), T.reshape(-1)
+        Wl = [W[so[b] + b:so[b + 1] + b + 1] for b in range(257)]
+        Tl = [T[so[b]:so[b + 1]] for b in range(257)]
+        EDl = list(np.random.default_rng(63).normal(scale=0.3, size=(257, 18)))
+        g = "r257" if ragged else "u257"
+        groups[g] = (Wl, Tl, None)
+        groups[g + "e"] = (Wl, Tl, EDl)
+    save_refine(groups)
 
 
 if __name__ == "__main__":

@@ -59,6 +59,7 @@ def test_status_strings_and_abi_version(lib):
     assert lib.tgms_abi_version() == 2
     assert lib.tgms_status_string(0) == b"TGMS_OK"
     assert lib.tgms_status_string(4) == b"TGMS_ERR_NO_DEVICE"
+    assert lib.tgms_status_string(7) == b"TGMS_ERR_SKIPPED"
     assert lib.tgms_status_string(99) == b"TGMS_ERR_UNKNOWN"
 
 

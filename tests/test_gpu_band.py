@@ -2,13 +2,12 @@
 partial pivoting in the segment-interleaved order, against the oracle's dense GEPP of
 the same permuted matrix (oracle KKT_BAND), the other formulations and the exact
 goldens.  Tolerance as everywhere: norm-wise per (trajectory, axis) <= 1e-9."""
-import glob
 import os
 
 import numpy as np
 import pytest
 
-from conftest import batch_rel_err
+from conftest import batch_rel_err, solve_goldens
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +70,7 @@ def test_band_ragged(band, oracle):
     assert batch_rel_err(so, C, R) <= TOL
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))))
+@pytest.mark.parametrize("path", solve_goldens())
 def test_band_goldens_exact(band, path):
     g = np.load(path)
     so = g["seg_offsets"]

@@ -239,12 +239,14 @@ def test_multi_error_path_leaves_handle_usable(solver, hook):
 def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
     """Round 5: tgms_refine_loop_multi_device does no pass over the offsets on the host; a
     trajectory with M outside 1..16 strictly inside a piece fails that piece on its device
-    (k_group_plan): the call returns OK, the piece's statuses are TGMS_ERR_INVALID_ARG with
-    zero coefficients and costs and the times kept, every other piece refines normally.  The
+    (k_group_plan): the call returns OK, the bad trajectory's status is TGMS_ERR_INVALID_ARG
+    and the rest of its piece TGMS_ERR_SKIPPED (round 6, ADVICE r05: the valid trajectories
+    of a failed piece are told apart from the bad one), all with zero coefficients and costs
+    and the times kept, every other piece refines normally.  The
     in-place handle (one device, no pipeline) is the single-device loop, which validates on
     the host and refuses the call."""
     import torch
-    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, TgmsError
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_SKIPPED, TgmsError
     from trajectory_generator_ros2_amd import synthetic as S
     so, W, T = S.ragged_batch(9000, 2, 16, seed=45)
     k = 4000
@@ -266,8 +268,9 @@ def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
     multi.refine_loop_multi_device(so, dso, dW, dT, 1.0, 0.1, 5, dC, dcost, dst)
     torch.cuda.synchronize()
     st, T1, C, cost = dst.cpu().numpy(), dT.cpu().numpy(), dC.cpu().numpy(), dcost.cpu().numpy()
-    bad = st == ERR_INVALID_ARG
-    assert bad[k] and 0 < bad.sum() < B and set(np.unique(st)) == {0, ERR_INVALID_ARG}
+    assert st[k] == ERR_INVALID_ARG and (st == ERR_INVALID_ARG).sum() == 1
+    bad = st != 0
+    assert 0 < bad.sum() < B and set(np.unique(st)) == {0, ERR_INVALID_ARG, ERR_SKIPPED}
     lo, hi = np.flatnonzero(bad)[[0, -1]]
     assert bad[lo:hi + 1].all()  # one contiguous piece
     segs_bad = np.zeros(Sg, bool)
@@ -285,8 +288,9 @@ def test_refine_multi_uniform_batch_takes_the_device_grouped_loop(oracle, with_e
     A uniform batch through the RCCL pipeline (self-gather) against the oracle: times and
     costs after 10 steps at the loop's amplification tolerance (as
     the configs' refinement tests), the final coefficients at north_star's 1e-9 on the GPU's
-    own times.  Tolerance after 10 steps: 1e-7, as test_gpu_configs.py's refinement tests
-    (the iterated map amplifies rounding; measured 1.3e-8 here, round 5)."""
+    own times.  Tolerance after 10 steps: 1e-9, as test_gpu_configs.py's refinement tests
+    (round 5 measured 1.3e-8 here against an oracle whose gradient was ~1e-8 off exact and
+    held it at 1e-7; the displacement-form oracle of round 6 agrees to ~1e-11)."""
     import torch
     from conftest import batch_rel_err
     from trajectory_generator_ros2_amd import synthetic as S
@@ -310,8 +314,8 @@ def test_refine_multi_uniform_batch_takes_the_device_grouped_loop(oracle, with_e
     Tg, Cg, cg = dT.cpu().numpy(), dC.cpu().numpy(), dcost.cpu().numpy()
     To, co, Co, sto = oracle.refine_batch(so, W, T, ED, 1.0, 0.1, 10, oracle.REDUCED)
     assert (sto == 0).all()
-    assert np.abs(Tg / To - 1).max() <= 1e-7
-    assert np.abs(cg / co - 1).max() <= 1e-7
+    assert np.abs(Tg / To - 1).max() <= 1e-9
+    assert np.abs(cg / co - 1).max() <= 1e-9
     R, rst = oracle.solve_batch(so, W, Tg, ED, oracle.REDUCED)
     assert (rst == 0).all()
     assert batch_rel_err(so, Cg, R) <= 1e-9

@@ -7,13 +7,12 @@ backend explicitly (`minsnap_backend: host`); tgms_create never falls back to it
 (tests/test_node_host.py::test_no_cpu_fallback).  Its solve is the product's own reduced
 formulation, held here to the oracle and the exact goldens at north_star's
 1e-9 (norm-wise per trajectory and axis), its sampler to the oracle's."""
-import glob
 import os
 
 import numpy as np
 import pytest
 
-from conftest import batch_rel_err
+from conftest import batch_rel_err, solve_goldens
 
 TOL = 1e-9
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -53,7 +52,7 @@ def test_host_ragged_vs_oracle(host, oracle):
     assert batch_rel_err(so, C, R) <= TOL
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))))
+@pytest.mark.parametrize("path", solve_goldens())
 def test_host_goldens_exact(host, path):
     g = np.load(path)
     so = g["seg_offsets"]

@@ -8,16 +8,15 @@ oracle is pinned by exact rational arithmetic instead:
   * closed-form single-segment KAT, linearity, translation, time reversal,
     collinearity and C6 smoothness.
 """
-import glob
 import os
 
 import numpy as np
 import pytest
 
-from conftest import batch_rel_err
+from conftest import batch_rel_err, solve_goldens
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-GOLDENS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+GOLDENS = solve_goldens()
 ORACLE_TOL = 1e-12   # dense KKT / square C6 oracle vs exact
 REDUCED_TOL = 1e-10  # reduced-Hessian restatement: knot derivatives -> monomials amplifies rounding
 

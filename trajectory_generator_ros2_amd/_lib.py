@@ -11,7 +11,7 @@ import os
 
 from .build import LIB_TGMS
 
-OK, ERR_INVALID_ARG, ERR_SINGULAR, ERR_NONFINITE, ERR_NO_DEVICE, ERR_DEVICE, ERR_UNSUPPORTED = range(7)
+OK, ERR_INVALID_ARG, ERR_SINGULAR, ERR_NONFINITE, ERR_NO_DEVICE, ERR_DEVICE, ERR_UNSUPPORTED, ERR_SKIPPED = range(8)
 METHOD_REDUCED, METHOD_DENSE_KKT, METHOD_BAND_KKT = 0, 1, 2
 YAW_CONSTANT, YAW_VELOCITY = 0, 1
 ABI_VERSION = 2

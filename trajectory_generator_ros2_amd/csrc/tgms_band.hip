@@ -357,7 +357,9 @@ __device__ __forceinline__ void quad_step(const int k, const int q0, double (&u)
         const uint32_t vrow5 = (q < 2) ? vrow1 + 32u : 0x7FFFFF00u;
         asm volatile("" ::"v"(vrow1), "v"(vrow5));
         __builtin_amdgcn_sched_barrier(0);
+#ifndef TGMS_BAND_NOGUARD  // diagnosis build: the unguarded form of round 5's failing builds
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[0], v[2])), rs, vrow, so, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(v[1], v[3])), rs, vrow + 64u, so, 0);
@@ -484,7 +486,9 @@ __device__ __forceinline__ void back_step(int k, int l0, int g, __amdgpu_buffer_
             // the same guard as quad_step's slab stores: the address is not a fresh VALU result
             asm volatile("" ::"v"(o));
             __builtin_amdgcn_sched_barrier(0);
+#ifndef TGMS_BAND_NOGUARD
             asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
             __builtin_amdgcn_sched_barrier(0);
             o[0] = emit ? -sm[0] : 0.0;
             o[8] = emit ? -sm[1] : 0.0;

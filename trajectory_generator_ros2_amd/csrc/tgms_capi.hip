@@ -89,6 +89,7 @@ struct tgms_handle {
         LoopKey key;
         hipGraphExec_t exec = nullptr;
         uint64_t used = 0;
+        hipEvent_t done = nullptr;  // recorded after every replay: eviction waits on it
     };
     std::vector<LoopGraph> loop_graphs;
     uint64_t loop_clock = 0;
@@ -484,6 +485,10 @@ tgms_status ensure_band(tgms_handle* h, int m_max, hipStream_t stream, double** 
             // orders the graphs' replays after it, so the host waits for it here -- on the
             // pinned completion word, not a HIP call (hipEventSynchronize inside a capture
             // invalidates it, round 5)
+            if (h->band_unmarked)  // cannot happen since every uncaptured band call releases
+                return set_err(h, TGMS_ERR_DEVICE,
+                               "an uncaptured band-KKT call ended without its completion marker; the capture "
+                               "cannot tell when the slab it takes over is free");
             if (h->band_done) {
                 const auto t0 = std::chrono::steady_clock::now();
                 while ((int32_t)(__atomic_load_n(h->band_done, __ATOMIC_ACQUIRE) - h->band_seq) < 0) {
@@ -654,19 +659,28 @@ tgms_status run_loop_graph(tgms_handle* h, const tgms_handle::LoopKey& key, hipS
         const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
         if (ei != hipSuccess) return hip_err(h, ei, "hipGraphInstantiate");
+        hipEvent_t done = nullptr;
+        const hipError_t ee = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+        if (ee != hipSuccess) {
+            (void)hipGraphExecDestroy(exec);
+            return hip_err(h, ee, "hipEventCreateWithFlags");
+        }
         if (h->loop_graphs.size() >= kLoopGraphs) {
             auto lru = std::min_element(h->loop_graphs.begin(), h->loop_graphs.end(),
                                         [](const auto& a, const auto& b) { return a.used < b.used; });
-            // the evicted graph may still be running: destroying an exec that has been
-            // launched is deferred by the runtime until its work completes
+            // the evicted graph may still be running (a replay on another stream, e.g. a
+            // multi-GPU piece on sc[d]): wait for its last replay before destroying it
+            TGMS_HIP(h, hipEventSynchronize(lru->done));
             TGMS_HIP(h, hipGraphExecDestroy(lru->exec));
+            TGMS_HIP(h, hipEventDestroy(lru->done));
             h->loop_graphs.erase(lru);
         }
-        h->loop_graphs.push_back({key, exec, 0});
+        h->loop_graphs.push_back({key, exec, 0, done});
         hit = &h->loop_graphs.back();
     }
     hit->used = ++h->loop_clock;
     TGMS_HIP(h, hipGraphLaunch(hit->exec, stream));
+    TGMS_HIP(h, hipEventRecord(hit->done, stream));
     return TGMS_OK;
 }
 
@@ -1084,7 +1098,10 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
             if (s != TGMS_OK) return s;
             s = dispatch(h, p0, b1, a.d_so, a.dW, a.dT, a.dED, a.dC, a.dSt, ustream);
         }
-        if (s == TGMS_OK) s = scratch_release(h, ustream);
+        {  // released on failure too: a band call that launched must still write its marker
+            const tgms_status r_ = scratch_release(h, ustream);
+            if (s == TGMS_OK) s = r_;
+        }
         if (s != TGMS_OK) return s;
     }
     // pieces: solve on the device, then gather to device 0 beside the next piece's solve
@@ -1231,6 +1248,7 @@ const char* tgms_status_string(int status) {
         case TGMS_ERR_NO_DEVICE: return "TGMS_ERR_NO_DEVICE";
         case TGMS_ERR_DEVICE: return "TGMS_ERR_DEVICE";
         case TGMS_ERR_UNSUPPORTED: return "TGMS_ERR_UNSUPPORTED";
+        case TGMS_ERR_SKIPPED: return "TGMS_ERR_SKIPPED";
         default: return "TGMS_ERR_UNKNOWN";
     }
 }
@@ -1291,8 +1309,11 @@ void tgms_destroy(tgms_handle* h) {
         if (h->join_ev[j]) (void)hipEventDestroy(h->join_ev[j]);
     }
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-    for (auto& g : h->loop_graphs)
+    for (auto& g : h->loop_graphs) {
+        if (g.done) (void)hipEventSynchronize(g.done);
         if (g.exec) (void)hipGraphExecDestroy(g.exec);
+        if (g.done) (void)hipEventDestroy(g.done);
+    }
     if (h->d_plan) (void)hipFree(h->d_plan);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1371,7 +1392,10 @@ tgms_status tgms_solve_batch(tgms_handle* h, int32_t B, const int32_t* so, const
     s = plan_upload(h, B, so, &plan, st);
     if (s != TGMS_OK) return s;
     s = dispatch(h, plan, B, dSo, dW, dT, dED, dC, dSt, st);
-    if (s == TGMS_OK) s = scratch_release(h, st);
+    {  // released on failure too: a band call that launched must still write its marker
+        const tgms_status r_ = scratch_release(h, st);
+        if (s == TGMS_OK) s = r_;
+    }
     if (s != TGMS_OK) return s;
     TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     std::vector<int32_t> hst;
@@ -1427,9 +1451,13 @@ tgms_status tgms_solve_uniform_device(tgms_handle* h, int32_t B, int32_t M, cons
         double* slab = nullptr;
         tgms_status s = ensure_band(h, M, st, &slab);
         if (s == TGMS_OK) s = scratch_acquire(h, st);
-        if (s != TGMS_OK) return s;
-        TGMS_HIP(h, tgms::launch_band_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, slab, h->band_grid, st));
-        return scratch_release(h, st);
+        if (s != TGMS_OK) {
+            if (!capturing(st)) (void)scratch_release(h, st);  // ensure_band may have armed the marker
+            return s;
+        }
+        const hipError_t e = tgms::launch_band_kkt(M, B, nullptr, nullptr, dW, dT, dED, dC, dSt, slab, h->band_grid, st);
+        const tgms_status r = scratch_release(h, st);
+        return e != hipSuccess ? hip_err(h, e, "launch_band_kkt") : r;
     } else if (h->method == TGMS_METHOD_REDUCED)
         TGMS_HIP(h, tgms::launch_reduced_uniform(M, B, dW, dT, dED, dC, dSt, st));
     else
@@ -1548,7 +1576,10 @@ tgms_status tgms_refine_batch(tgms_handle* h, int32_t B, const int32_t* so, cons
     int cur = 0;
     s = refine_loop(h, plan, B, (int64_t)S, dSo, dW, dT, dED, k_T, eta, iters, coeffs ? dC : nullptr, dCost, dSt, st,
                     &cur, &dp);
-    if (s == TGMS_OK) s = scratch_release(h, st);
+    {  // released on failure too: a band call that launched must still write its marker
+        const tgms_status r_ = scratch_release(h, st);
+        if (s == TGMS_OK) s = r_;
+    }
     if (s != TGMS_OK) return s;
     if (coeffs) TGMS_HIP(h, hipMemcpyAsync(coeffs, dC, nC * 8, hipMemcpyDeviceToHost, st));
     TGMS_HIP(h, hipMemcpyAsync(seg_times, dT[cur], S * 8, hipMemcpyDeviceToHost, st));
@@ -1586,7 +1617,8 @@ tgms_status tgms_refine_loop_device(tgms_handle* h, int32_t B, const int32_t* h_
     if (s == TGMS_OK) s = scratch_acquire(h, st);
     if (s != TGMS_OK) return s;
     s = loop_on_device(h, B, (int64_t)h_so[B], um, d_so, dW, dT, dED, k_T, eta, iters, dC, d_cost, dSt, st);
-    return s != TGMS_OK ? s : scratch_release(h, st);
+    const tgms_status r = scratch_release(h, st);  // on failure too (the band marker)
+    return s != TGMS_OK ? s : r;
 }
 
 int64_t tgms_sample_count(double total_T, double dt) {

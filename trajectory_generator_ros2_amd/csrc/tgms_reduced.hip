@@ -2003,8 +2003,9 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter_dev(int32_t B, cons
 // workgroup sums them per M (16 bins x 64 strided partial sums), checks the offsets against
 // the host's B and S, and thread 0 lays out the starts and both classes' group tables in
 // the order the host planner used (M descending within a class).  A bad plan runs nothing
-// and marks every trajectory TGMS_ERR_INVALID_ARG, its outputs exact zeros (rare path: one
-// workgroup clears the S x 24 coefficients).
+// and marks the trajectories whose own M is outside 1..16 TGMS_ERR_INVALID_ARG and the
+// others TGMS_ERR_SKIPPED, all outputs exact zeros (rare path: one workgroup clears the
+// S x 24 coefficients).
 constexpr int PLAN_THREADS = 1024;
 __global__ __launch_bounds__(PLAN_THREADS) void k_group_plan(int32_t n, int64_t S, const int32_t* __restrict__ so,
                                                             int has_ed, const int32_t* __restrict__ hist,
@@ -2064,7 +2065,8 @@ __global__ __launch_bounds__(PLAN_THREADS) void k_group_plan(int32_t n, int64_t 
     __syncthreads();
     if (!bad_s) return;
     for (int64_t b = t; b < n; b += PLAN_THREADS) {
-        if (status) status[b] = TGMS_ERR_INVALID_ARG;
+        const int64_t m = (int64_t)so[b + 1] - so[b];
+        if (status) status[b] = (m < 1 || m > TGMS_MAX_SEGMENTS) ? TGMS_ERR_INVALID_ARG : TGMS_ERR_SKIPPED;
         if (cost) cost[b] = 0.0;
     }
     if (C)
