@@ -51,18 +51,20 @@ def refine_flops_per_traj(M: int, iters: int = 10) -> float:
     """Algorithmic FP64 flops of one config-5 call per trajectory: the
     one-sided block LDL^T of DESIGN.md §2 over the M - 1 interior knots, three axes, counted
     operation by operation (an FMA is 2 flops; a reciprocal 1), `iters` passes that end in the
-    cost and its T-derivative per segment-axis (seg_cost_p) plus the update, and one pass that
-    ends in the coefficients and the cost (seg_cost_q).  Per interior knot: powers 6, the
-    diagonal block 18, the coupling 9, G = S^-1 C 45 and the Schur update 36 (from the second
-    knot on), the 3x3 LDL^T 14; per knot and axis: right-hand side 11, forward 33, back 18.
-    Per segment and axis: the Hermite -> P4..P7 map 58, then cost + gradient 84, or the
-    coefficients 4 + cost 27; per segment the update 8.  This is what the algorithm needs,
-    not what the lane-pair kernels execute (their twisted interface and duplicated blocks
-    are in the executed count beside it)."""
+    cost and its T-derivative per segment-axis plus the update, and one pass that ends in the
+    coefficients and the cost (seg_cost_q).  Per interior knot: powers 6, the diagonal block
+    18, the coupling 9, G = S^-1 C 45 and the Schur update 36 (from the second knot on), the
+    3x3 LDL^T 14; per knot and axis: right-hand side 11, forward 33, back 18.  Per segment and
+    axis in a gradient pass (round 6: the Legendre-basis form, seg_grad_u): the scaled end
+    data 6, cost and gradient 44, accumulation 4 (round 5's count, for the P4..P7 form it
+    replaced: 58 + 84); in the last pass the Hermite -> P4..P7 map 58, the coefficients 4 and
+    the cost 27; per segment the powers r^2, r^3 2 and the update 8.  This is what the
+    algorithm needs, not what the lane-pair kernels execute (their twisted interface and
+    duplicated blocks are in the executed count beside it)."""
     nk = M - 1
     fac = nk * (6 + 18 + 9 + 14) + max(nk - 1, 0) * (45 + 36)
     sub = 3 * (nk * (11 + 18) + nk * 15 + max(nk - 1, 0) * 18)
-    grad_pass = fac + sub + M * 3 * (58 + 84) + M * 8
+    grad_pass = fac + sub + M * 3 * (6 + 44 + 4) + M * (2 + 8)
     final_pass = fac + sub + M * 3 * (58 + 4 + 27)
     return float(iters * grad_pass + final_pass)
 
@@ -188,7 +190,11 @@ def cpu_baseline(B: int, M: int, target_s: float, check=None):
 
 
 C5_PMC_FILE = "profiles/c5_pmc.json"
-BYTE_MIX_FLOOR_US = 28.6  # config 3's byte mix with no compute, best occupancy (profiles/archive/r03_runstore_occ.txt)
+BYTE_MIX_FLOOR_US = 28.6  # config 3's byte mix with no compute, best occupancy (profiles/archive/r03_runstore_occ.txt;
+#                            round 6 on another box: 29.1 us, profiles/r06_floor.jsonl -- the lower one is kept)
+# the same bytes with consecutive launches overlapping over 4 streams in one graph, best occupancy
+# (scripts/micro/floor.hip, profiles/r06_floor.jsonl): the floor of the headline's pipelined region
+PIPELINED_FLOOR_US = 27.4
 
 
 def _c5_shard(so_all, W_all, T_all, bounds, part, dev):
@@ -937,7 +943,9 @@ def main():
                          "batches) alternate between them, one handle each, so a step's loads and "
                          "factorisation overlap the previous step's store drain; 1: steps back to back. The "
                          "roofline is timed separately with one stream (kernel durations, as rocprofv3 sees them)")
-    ap.add_argument("--dense-steps", type=int, default=3, help="steps of the dense-KKT side line (0: skip)")
+    ap.add_argument("--dense-steps", type=int, default=1,
+                    help="steps of the dense-KKT side line (0: skip).  The dense KKT is a cross-check method "
+                         "(DESIGN.md section 4): one timing")
     ap.add_argument("--band-steps", type=int, default=5, help="steps of the band-KKT side line (0: skip)")
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
@@ -1271,7 +1279,13 @@ def main():
                          # the headline region itself: steps overlapping across the streams
                          "pipelined": {"streams": nstreams, "ms_per_step_events": step_ms_max,
                                        "achieved": bpl / (step_ms_max * 1e-3) / 1e9,
-                                       "frac": bpl / (step_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+                                       "frac": bpl / (step_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                       "floor_us": PIPELINED_FLOOR_US if (B, M) == (65536, 10) and nstreams > 1
+                                       else None,
+                                       "floor_frac": (PIPELINED_FLOOR_US / (step_ms_max * 1e3))
+                                       if (B, M) == (65536, 10) and nstreams > 1 else None,
+                                       "floor_source": "profiles/r06_floor.jsonl (scripts/micro/floor.hip: the same "
+                                                       "bytes, no compute, 4 streams in one graph, best occupancy)"}},
             # the timed region's own output: every set reset to NaN /
             # status -1 before it, then bit-compared with a one-stream re-solve and (set 0,
             # rank 0) with the CPU baseline's oracle output

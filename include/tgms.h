@@ -229,9 +229,12 @@ tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t part
  * device, device 0 -> dev), then gather groups 4..7 (piece k's results, dev -> device 0);
  * each transfer is one ncclSend on one side and one ncclRecv on the other.  flags:
  * TGMS_SCHED_* below.  Returns TGMS_ERR_INVALID_ARG (with *n_pieces / *n_xfers set to the
- * sizes needed) when piece_cap or xfer_cap is too small.  With TGMS_SCHED_REFINE it does
- * exactly the host work of tgms_refine_loop_multi_device before its first transfer (no pass
- * over the offsets; the cuts checked); without, the solve's validation pass as well. */
+ * sizes needed) when piece_cap or xfer_cap is too small.  It does exactly the host work of
+ * the call before its first transfer.  With TGMS_SCHED_REFINE: no pass over the offsets
+ * (the cuts checked).  Without (a solve): for the reduced method the offsets' ends and a
+ * uniform check that stops at the first 4,096-trajectory block holding two different M (a
+ * ragged batch is then grouped and checked per trajectory on its devices, as a refinement
+ * loop's; round 6); for the band / dense methods the full validation pass. */
 #define TGMS_SCHED_REFINE 1
 #define TGMS_SCHED_END_DERIVS 2
 #define TGMS_SCHED_COEFFS 4
@@ -241,15 +244,16 @@ tgms_status tgms_plan_shards(int32_t B, const int32_t* seg_offsets, int32_t part
 typedef struct tgms_piece {
     int32_t dev, piece, lo, hi; /* trajectories [lo, hi) */
     int64_t s0, s1;             /* segments [s0, s1) */
-    int64_t ws_off[11];         /* byte offsets: seg_offsets (ragged: rebased for a solve, the raw slice
-                                   for a refinement loop), permutation, W, T, T2, ED, C, status, cost,
-                                   and for a ragged refinement loop the device grouping's block counts
-                                   and its device-side plan (uniform batches: empty regions) */
+    int64_t ws_off[11];         /* byte offsets: seg_offsets (ragged: rebased for a band / dense solve,
+                                   the raw slice for a refinement loop or a reduced solve),
+                                   permutation, W, T, T2, ED, C, status, cost, and for a device-planned
+                                   piece the device grouping's block counts and its device-side plan
+                                   (uniform batches: empty regions) */
 } tgms_piece;
 typedef struct tgms_xfer {
     int32_t dev, piece, gather; /* gather 0: device 0 -> dev (scatter), 1: dev -> device 0 */
     int32_t array;              /* 0 W, 1 T, 2 end derivs, 3 coeffs, 4 status, 5 cost, 6 seg_offsets
-                                   (the slice [lo, hi] of a ragged refinement loop's piece) */
+                                   (the slice [lo, hi] of a device-planned piece) */
     int64_t batch_elem;         /* element offset in the device-0 batch array */
     int64_t ws_byte;            /* byte offset in dev's piece workspace */
     int64_t count;              /* elements */
@@ -264,7 +268,13 @@ tgms_status tgms_multi_schedule(int32_t device_count, int32_t B, const int32_t* 
 tgms_status tgms_solve_batch_multi(tgms_handle* h, int32_t B, const int32_t* seg_offsets,
                                    const double* waypoints, const double* seg_times,
                                    const double* end_derivs, double* coeffs, int32_t* status);
-/* Device-0 pointers, asynchronous on `stream` (a device-0 stream). */
+/* Device-0 pointers, asynchronous on `stream` (a device-0 stream).  Reduced method, ragged
+ * batch (round 6): the host reads only the offsets' ends and the shard / piece cuts; every
+ * device groups and checks its pieces' trajectories (as tgms_refine_loop_multi_device): a
+ * trajectory with M outside 1..16 fails its piece -- TGMS_ERR_INVALID_ARG for it,
+ * TGMS_ERR_SKIPPED for the piece's others, zero coefficients -- and the call returns
+ * TGMS_OK, so check d_status.  Band / dense methods and uniform batches are validated on the
+ * host as before (an error return names the first offending trajectory). */
 tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32_t* h_seg_offsets,
                                           const int32_t* d_seg_offsets, const double* d_waypoints,
                                           const double* d_seg_times, const double* d_end_derivs,

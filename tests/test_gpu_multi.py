@@ -281,6 +281,56 @@ def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
     assert not np.array_equal(T1[~segs_bad], T[~segs_bad])
 
 
+def test_solve_multi_ragged_bad_offsets_fail_on_the_device(multi, request):
+    """Round 6: a ragged reduced solve over the multi-GPU path no longer
+    scans the offsets on the host -- each piece (and device 0's shard) is grouped on its
+    device (k_perm_hist -> k_group_plan -> k_perm_scatter_dev -> k_reduced_multi_dev).  A
+    trajectory with M outside 1..16 strictly inside the batch: the call returns OK, that
+    trajectory reads TGMS_ERR_INVALID_ARG, the rest of its piece (or of device 0's shard)
+    TGMS_ERR_SKIPPED, all with zero coefficients; every other trajectory equals the
+    single-device solve bit for bit."""
+    import torch
+    from trajectory_generator_ros2_amd import ERR_INVALID_ARG, ERR_SKIPPED
+    from trajectory_generator_ros2_amd import synthetic as S
+    from trajectory_generator_ros2_amd.solver import Solver
+    so, W, T = S.ragged_batch(9000, 2, 16, seed=46)
+    k = 4000
+    so = so.astype(np.int32).copy()
+    so[k + 1:] += 20  # trajectory k: M + 20 segments (W / T padded with valid values)
+    B, Sg = len(so) - 1, int(so[-1])
+    T = np.concatenate([T, np.full(20, 0.7)])
+    W = np.concatenate([W, np.random.default_rng(2).normal(size=(20, 3))])
+    d = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dso, dW, dT = d(so), d(W), d(T)
+    dC = torch.full((Sg, 3, 8), float("nan"), dtype=torch.float64, device="cuda")
+    dst = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    multi.solve_batch_multi_device(so, dso, dW, dT, dC, dst)
+    torch.cuda.synchronize()
+    st, C = dst.cpu().numpy(), dC.cpu().numpy()
+    assert st[k] == ERR_INVALID_ARG and (st == ERR_INVALID_ARG).sum() == 1
+    bad = st != 0
+    lo, hi = np.flatnonzero(bad)[[0, -1]]
+    assert bad[lo:hi + 1].all() and lo <= k <= hi  # one contiguous piece (or shard)
+    if request.node.callspec.params["multi"]:  # self-gather: a piece, not the whole batch
+        assert bad.sum() < B and set(np.unique(st)) == {0, ERR_INVALID_ARG, ERR_SKIPPED}
+    else:  # in place on one device: device 0's shard is the whole batch
+        assert bad.all() and set(np.unique(st)) == {ERR_INVALID_ARG, ERR_SKIPPED}
+    segs_bad = np.zeros(Sg, bool)
+    segs_bad[so[lo]:so[hi + 1]] = True
+    assert not C[segs_bad].any()
+    # the good trajectories: the single-device solve of the batch without the bad piece
+    good = np.flatnonzero(~bad)
+    with Solver(0) as one:
+        for a, b in ((0, lo), (hi + 1, B)):
+            if b <= a:
+                continue
+            so_l = (so[a:b + 1] - so[a]).astype(np.int32)
+            R, rst, _ = one.solve(so_l, W[so[a] + a:so[b] + b + 1], T[so[a]:so[b]])
+            assert (rst == 0).all()
+            np.testing.assert_array_equal(C[so[a]:so[b]], R)
+    assert len(good) + (hi + 1 - lo) == B
+
+
 @pytest.mark.parametrize("with_ed", [False, True])
 def test_refine_multi_uniform_batch_takes_the_device_grouped_loop(oracle, with_ed):
     """Round 5: tgms_refine_loop_multi_device runs every batch, uniform ones too, through the

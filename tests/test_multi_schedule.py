@@ -50,13 +50,14 @@ FLAGS = [SOLVE, SOLVE | S.SCHED_END_DERIVS, SOLVE | S.SCHED_SELF_GATHER, REFINE,
          S.SCHED_STATUS]
 
 
-def _region_sizes(p, flags, ragged):
+def _region_sizes(p, flags, ragged, method=0):
     """Bytes of ws_off[0..10]: offsets, permutation (ragged only), W, T, T2, ED, C, status,
-    cost, and for a refinement loop the device grouping's block counts and plan (round 5: every
-    refinement batch, uniform ones too, is grouped on the device, laid out as a ragged one)."""
+    cost, and for a device-planned piece the device grouping's block counts and plan (round 5:
+    every refinement batch, uniform ones too, is grouped on the device, laid out as a ragged
+    one; round 6: so is a ragged solve with the reduced method, method 0)."""
     n, Sg = p["hi"] - p["lo"], p["s1"] - p["s0"]
     refine = bool(flags & S.SCHED_REFINE)
-    dev = refine
+    dev = refine or (ragged and method == 0)
     ragged = ragged or refine
     return [4 * (n + 1) if ragged else 0, 4 * n if ragged else 0, 8 * 3 * (Sg + n), 8 * Sg, 8 * Sg if refine else 0,
             8 * 18 * n if flags & S.SCHED_END_DERIVS else 0, 8 * 24 * Sg if flags & S.SCHED_COEFFS else 0,
@@ -127,6 +128,8 @@ def test_schedule_structure(lib, n, flags):
             if flags & S.SCHED_REFINE:
                 want += [(1, 1), (1, 5)] if flags & S.SCHED_COST else [(1, 1)]
                 want += [(0, 6)]  # the offsets slice, planned on the device (uniform batches too)
+            elif ragged:
+                want += [(0, 6)]  # round 6: a ragged reduced solve is planned on the device too
             assert arrs == sorted(want), (name, arrs)
 
 
@@ -161,7 +164,8 @@ def test_schedule_executes_to_the_whole_batch_result(lib, n, self_gather):
     bounds, ws, P, X = multi_schedule(so, n, 0, flags)
     Cref, stref = _fake_solve(so, W, T)
     batch = {0: W.copy().view(np.uint8).reshape(-1), 1: T.copy().view(np.uint8).reshape(-1),
-             3: np.zeros(Cref.size * 8, np.uint8), 4: np.zeros(stref.size * 4, np.uint8)}
+             3: np.zeros(Cref.size * 8, np.uint8), 4: np.zeros(stref.size * 4, np.uint8),
+             6: so.astype(np.int32).view(np.uint8).reshape(-1)}
     written = {3: np.zeros(Cref.size, np.int32), 4: np.zeros(stref.size, np.int32)}
     wsb = [np.zeros(int(w), np.uint8) for w in ws]
     for x in [x for x in X if not x["gather"]]:
@@ -173,6 +177,9 @@ def test_schedule_executes_to_the_whole_batch_result(lib, n, self_gather):
         w = wsb[p["dev"]]
         npc, Sg = p["hi"] - p["lo"], p["s1"] - p["s0"]
         so_l = so[p["lo"]:p["hi"] + 1] - so[p["lo"]]
+        # the raw offsets slice the device plans from arrived with the inputs (round 6)
+        raw = w[p["ws_off"][0]:][:4 * (npc + 1)].view(np.int32)
+        np.testing.assert_array_equal(raw - raw[0], so_l)
         Wl = w[p["ws_off"][2]:][:8 * 3 * (Sg + npc)].view(np.float64).reshape(-1, 3)
         Tl = w[p["ws_off"][3]:][:8 * Sg].view(np.float64)
         Cl, stl = _fake_solve(so_l, Wl, Tl)
@@ -220,9 +227,10 @@ def test_refine_schedule_leaves_per_trajectory_checks_to_the_devices(lib):
     bad = so.copy()
     bad[1001:] += 20  # trajectory 1000 gets M + 20
     with pytest.raises(TgmsError):
-        multi_schedule(bad, 4, 0, SOLVE)
-    b, _, P, _ = multi_schedule(bad, 4, 0, REFINE)
-    assert not any(p["lo"] == 1000 or p["hi"] == 1001 for p in P)  # strictly inside a piece
+        multi_schedule(bad, 4, 2, SOLVE)  # band method: host-planned pieces, validated on the host
+    for flags in (REFINE, SOLVE):  # round 6: a reduced ragged solve leaves it to the devices too
+        b, _, P, _ = multi_schedule(bad, 4, 0, flags)
+        assert not any(p["lo"] == 1000 or p["hi"] == 1001 for p in P)  # strictly inside a piece
     for so_dec in ([0, 2, 4, 6, 3, 10, 12, 14, 16], [0, 2, 4, 1, 8, 10, 12, 14, 16]):
         b, _, P, _ = multi_schedule(np.array(so_dec, np.int32), 4, 0, REFINE)
         for q in P:
@@ -259,8 +267,10 @@ def test_schedule_host_time_at_8_devices(lib):
     before its first RCCL transfer -- the offsets' ends and cuts, the whole schedule (shards
     and pieces by binary search, workspaces, transfers) -- for 1,048,576 ragged trajectories
     over 8 devices, timed on the C call alone (tgms_multi_schedule with TGMS_SCHED_REFINE
-    runs exactly that work): median <= 0.1 ms.  The solve's schedule keeps its validation
-    pass (printed beside)."""
+    runs exactly that work): median <= 0.1 ms.  Round 6: the reduced
+    solve's schedule as well (its pieces are grouped on the devices; round 5 kept a
+    validation pass, 0.71 ms); the band method's, which keeps it, and a uniform batch's
+    detection pass are printed beside."""
     import ctypes
     import time
     from trajectory_generator_ros2_amd import _lib
@@ -283,6 +293,20 @@ def test_schedule_host_time_at_8_devices(lib):
         return sorted(ts)[15]
     refine = med(REFINE | 4 | 8 | 16)
     solve = med(SOLVE | 4 | 8)
-    print(f"tgms_multi_schedule n=8 B=1,048,576 ragged: refinement loop {refine * 1e3:.4f} ms "
-          f"({npc.value} pieces, {nx.value} transfers), solve (validation pass) {solve * 1e3:.3f} ms")
+
+    def med_m(flags, so_, method):
+        ts = []
+        for _ in range(11):
+            t0 = time.perf_counter()
+            st = lib.tgms_multi_schedule(n, len(so_) - 1, ptr(so_), method, flags, ptr(bounds), ptr(ws), pieces, 64,
+                                         ctypes.byref(npc), xfers, 1024, ctypes.byref(nx))
+            ts.append(time.perf_counter() - t0)
+            assert st == 0
+        return sorted(ts)[5]
+    band = med_m(SOLVE | 4 | 8, so, 2)
+    uni = med_m(SOLVE | 4 | 8, SY.uniform_batch(1 << 20, 10)[0].astype(np.int32), 0)
+    print(f"tgms_multi_schedule n=8 B=1,048,576 ragged: refinement loop {refine * 1e3:.4f} ms, reduced solve "
+          f"{solve * 1e3:.4f} ms ({npc.value} pieces, {nx.value} transfers); band solve (validation pass) "
+          f"{band * 1e3:.3f} ms; uniform M=10 reduced solve (uniform detection) {uni * 1e3:.3f} ms")
     assert refine <= 1e-4
+    assert solve <= 1e-4

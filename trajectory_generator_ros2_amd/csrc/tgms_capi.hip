@@ -633,6 +633,59 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, int64_t S, con
     return TGMS_OK;
 }
 
+// A ragged solve (reduced method) grouped on the device (round 6): k_perm_hist ->
+// k_group_plan -> k_perm_scatter_dev, then both occupancy classes from the device plan, so
+// the host makes no pass over the offsets.  A bad M fails the batch on the device
+// (TGMS_ERR_INVALID_ARG where M is outside 1..16, TGMS_ERR_SKIPPED elsewhere, zeros).
+tgms_status solve_ragged_dev(tgms_handle* h, int32_t B, int64_t S, const int32_t* d_so, const double* W,
+                             const double* T, const double* ED, double* C, int32_t* st, hipStream_t stream,
+                             const DevPlanBufs& dp) {
+    if (B <= 0) return TGMS_OK;
+    if (!dp.hist || !dp.perm || !dp.plan) return set_err(h, TGMS_ERR_DEVICE, "internal: ragged solve without plan buffers");
+    TGMS_HIP(h, tgms::launch_group_plan_dev(B, S, d_so, ED != nullptr, dp.hist, dp.perm, dp.plan, st, C, nullptr,
+                                            stream));
+    std::vector<std::function<hipError_t(hipStream_t)>> jobs;
+    for (int k = 1; k >= 0; --k)
+        jobs.push_back([&, k](hipStream_t q) {
+            return tgms::launch_reduced_multi_dev(k, B, dp.plan, d_so, W, T, ED, C, st, q);
+        });
+    return run_parallel(h, stream, jobs);
+}
+
+// so[b] == M0 b for every b <= B (so[0] == 0 and so[B] within [B, 16 B] checked by the
+// caller): one load per trajectory against an induction variable, in blocks of 4,096 that
+// stop at the first block holding a different M.  Modulo 2^32 is exact here: offsets in
+// [0, 2^31) congruent to M0 b for every b step by exactly M0.
+bool uniform_offsets(int32_t B, const int32_t* so, int32_t M0) {
+    const uint32_t m = (uint32_t)M0;
+    uint32_t diff = 0;
+    for (int32_t b0 = 0; b0 <= B && diff == 0; b0 += 4096) {
+        const int32_t e = std::min(B + 1, b0 + 4096);
+        for (int32_t b = b0; b < e; ++b) diff |= (uint32_t)so[b] ^ (m * (uint32_t)b);
+    }
+    return diff == 0;
+}
+
+// The host check of a multi-GPU ragged solve with the reduced method (round 6, as the
+// refinement loop's): the offsets' ends, and uniform detection in blocks of 4,096 that stops
+// at the first block holding two different M (a ragged batch leaves after its first block).
+// A uniform batch keeps the uniform kernels (its M checked here); a ragged one is grouped
+// and checked per trajectory on its devices.
+tgms_status scan_multi_offsets(tgms_handle* h, int32_t B, const int32_t* so, int max_m, int* uniform_m) {
+    if (B < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "B < 0");
+    if (!so) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets is NULL");
+    if (so[0] != 0) return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets[0] != 0");
+    *uniform_m = 0;
+    if (B == 0) return TGMS_OK;
+    if (so[B] < B || (int64_t)so[B] > (int64_t)TGMS_MAX_SEGMENTS * B)
+        return set_err(h, TGMS_ERR_INVALID_ARG, "seg_offsets[B] outside [B, 16 B]");
+    const int32_t M0 = so[1] - so[0];
+    if (!uniform_offsets(B, so, M0)) return TGMS_OK;
+    if (M0 < 1 || M0 > max_m) return set_err(h, TGMS_ERR_INVALID_ARG, "uniform batch with M outside the method's range");
+    *uniform_m = M0;
+    return TGMS_OK;
+}
+
 // Replay the handle's graph for `key`, capturing `body` into it first if there is none
 // (at most kLoopGraphs cached per handle, least recently used evicted).  Runs on the
 // handle's device (the caller has selected it).
@@ -948,6 +1001,9 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
     const bool refine = a.job == MultiJob::Refine;
     const int max_m = refine ? TGMS_MAX_SEGMENTS : max_m_for(h);
     const int um = a.checked ? a.checked->uniform_m : 0;
+    // a ragged solve with the reduced method: every piece (and device 0's shard) grouped on
+    // its device, as the refinement loop's (round 6)
+    const bool dev_solve = !refine && h->method == TGMS_METHOD_REDUCED && um <= 0;
     // the whole schedule (shards, pieces, workspace layout, transfers) from the host-only
     // planner (tgms_plan.cpp, CPU-tested through tgms_multi_schedule)
     tgms::MultiFlags fl;
@@ -1086,6 +1142,11 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
             // start at 0: shard 0 is the batch's first trajectories)
             s = loop_on_device(h, b1, (int64_t)a.h_so[b1], um, a.d_so, a.dW, a.dT, a.dED, a.k_T, a.eta, a.iters,
                                a.dC, a.d_cost, a.dSt, ustream);
+        } else if (dev_solve) {
+            s = ensure_perm_device(h, b1);
+            if (s == TGMS_OK)
+                s = solve_ragged_dev(h, b1, (int64_t)a.h_so[b1], a.d_so, a.dW, a.dT, a.dED, a.dC, a.dSt, ustream,
+                                     DevPlanBufs{h->d_perm_hist, h->d_perm, h->d_plan});
         } else {
             Plan p0;
             if (a.checked && b1 == a.B) {  // the whole batch on device 0: validated already
@@ -1143,6 +1204,12 @@ tgms_status multi_enqueue(tgms_handle* h, const MultiArgs& a, hipStream_t ustrea
                 const tgms_handle::LoopKey key{np, a.iters, Sp, so_p, Wp, Tp, T[1], EDp, Cp, costp, Stp, dp.perm,
                                                dp.hist, dp.plan, a.k_T, a.eta, pl.uniform_m};
                 s = run_loop_graph(hd, key, m->sc[d], body);
+            } else if (dev_solve) {
+                // planned on the device from the raw offsets slice that arrived with its inputs
+                s = solve_ragged_dev(hd, p.n(), p.S(), so_p, Wp, Tp, EDp, Cp, Stp, m->sc[d],
+                                     DevPlanBufs{reinterpret_cast<int32_t*>(w + p.oHist),
+                                                 reinterpret_cast<int32_t*>(w + p.oPerm),
+                                                 reinterpret_cast<tgms::DevPlan*>(w + p.oPlan)});
             } else {
                 s = dispatch(hd, plans[d][k], p.n(), so_p, Wp, Tp, EDp, Cp, Stp, m->sc[d]);
             }
@@ -1767,6 +1834,14 @@ tgms_status tgms_multi_schedule(int32_t device_count, int32_t B, const int32_t* 
         // as tgms_refine_loop_multi_device: no pass over the offsets (the devices check each
         // trajectory's M), every batch on the device-grouped loop; the cuts are checked below
         if (B > 0 && (so[B] < B || (int64_t)so[B] > (int64_t)TGMS_MAX_SEGMENTS * B)) return TGMS_ERR_INVALID_ARG;
+    } else if (method == TGMS_METHOD_REDUCED) {
+        // as tgms_solve_batch_multi_device (scan_multi_offsets): the ends, and uniform
+        // detection that stops at the first block with two different M
+        if (B > 0 && (so[B] < B || (int64_t)so[B] > (int64_t)TGMS_MAX_SEGMENTS * B)) return TGMS_ERR_INVALID_ARG;
+        const int32_t m0 = B > 0 ? so[1] - so[0] : 0;
+        const bool uni = B > 0 && uniform_offsets(B, so, m0);
+        if (uni && (m0 < 1 || m0 > TGMS_MAX_SEGMENTS)) return TGMS_ERR_INVALID_ARG;
+        M0 = uni ? m0 : 0;
     } else {
         int32_t lo = INT32_MAX, hi = INT32_MIN;  // one vectorised pass (as scan_offsets)
         for (int32_t b = 0; b < B; ++b) {
@@ -1823,7 +1898,11 @@ tgms_status tgms_solve_batch_multi_device(tgms_handle* h, int32_t B, const int32
     if (!h->multi) return tgms_solve_batch_device(h, B, h_so, d_so, dW, dT, dED, dC, dSt, stream);
     h->last_error.clear();
     Plan checked;
-    tgms_status s = check_offsets(h, B, h_so, max_m_for(h), &checked.counts, &checked.uniform_m);
+    // reduced method: no pass over a ragged batch's offsets on the host (its devices group and
+    // check it, include/tgms.h); band / dense: the host-planned pieces need the validated counts
+    tgms_status s = h->method == TGMS_METHOD_REDUCED
+                        ? scan_multi_offsets(h, B, h_so, max_m_for(h), &checked.uniform_m)
+                        : check_offsets(h, B, h_so, max_m_for(h), &checked.counts, &checked.uniform_m);
     if (s != TGMS_OK || B == 0) return s;
     if (!d_so || !dW || !dT || !dC) return set_err(h, TGMS_ERR_INVALID_ARG, "NULL device pointer");
     TGMS_CHECK_ALIGNED(h, dW, dT, dED, dC);

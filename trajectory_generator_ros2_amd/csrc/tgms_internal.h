@@ -109,6 +109,10 @@ hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int ha
 hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
                                   double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
                                   double* C, int32_t* status, hipStream_t stream);
+// The ragged solve of one occupancy class from a device plan (k_reduced_multi's blocks).
+hipError_t launch_reduced_multi_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+                                    const double* T, const double* ED, double* C, int32_t* status,
+                                    hipStream_t stream);
 
 // Sampler: one workgroup per trajectory (grid-stride), 14 doubles per sample.
 hipError_t launch_sample(int32_t B, const int32_t* seg_offsets, const double* W, const double* T,

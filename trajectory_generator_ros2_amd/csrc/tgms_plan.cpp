@@ -118,10 +118,11 @@ void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, 
             plan_shards(hi - lo, nullptr, MULTI_PIECES, method, pb, uniform_m);
         else
             plan_shards(hi - lo, so + lo, MULTI_PIECES, method, pb);  // the shard's slice, no copy
-        // ragged solve: host-planned pieces (plan block uploaded); ragged refinement loop:
-        // planned on the device (offsets slice scattered with the inputs)
-        const bool host_plan = uniform_m <= 0 && !f.refine;
-        const bool dev_plan = uniform_m <= 0 && f.refine;
+        // ragged refinement loop and (round 6) ragged reduced solve: planned on the device
+        // (offsets slice scattered with the inputs); ragged band / dense solve: host-planned
+        // pieces (plan block uploaded)
+        const bool dev_plan = uniform_m <= 0 && (f.refine || method == TGMS_METHOD_REDUCED);
+        const bool host_plan = uniform_m <= 0 && !dev_plan;
         std::vector<PiecePlan>& ps = P.pieces[d];
         size_t plan_bytes = 0;
         for (int k = 0; k < MULTI_PIECES; ++k) {
@@ -172,7 +173,7 @@ void plan_multi(int n, int32_t B, const int32_t* so, int method, int uniform_m, 
             P.xfers.push_back({d, k, 0, XA_W, (p.s0 + p.lo) * 3, (int64_t)p.oW, (p.S() + p.n()) * 3, 8, k});
             P.xfers.push_back({d, k, 0, XA_T, p.s0, (int64_t)p.oT, p.S(), 8, k});
             if (f.has_ed) P.xfers.push_back({d, k, 0, XA_ED, (int64_t)p.lo * 18, (int64_t)p.oED, (int64_t)p.n() * 18, 8, k});
-            if (f.refine && uniform_m <= 0)  // the raw offsets slice for the device-side plan
+            if (uniform_m <= 0 && (f.refine || method == TGMS_METHOD_REDUCED))  // the raw offsets slice, device-planned
                 P.xfers.push_back({d, k, 0, XA_SO, (int64_t)p.lo, (int64_t)p.oSo, (int64_t)p.n() + 1, 4, k});
         }
     for (int k = 0; k < MULTI_PIECES; ++k)

@@ -53,6 +53,11 @@ namespace {
 #ifndef TGMS_JOINT_AXES
 #define TGMS_JOINT_AXES 1
 #endif
+// The refinement gradient in the Legendre basis of the snap (seg_grad_u, round 6); 0: round
+// 5's P4..P7 + seg_cost_p form (A/B builds).
+#ifndef TGMS_GRAD_LEGENDRE
+#define TGMS_GRAD_LEGENDRE 1
+#endif
 
 // Scheduling fence between unrolled chain / emission steps.  The compiler-level
 // memory clobber also stops CSE of LDS reads across steps: re-reading LDS is far
@@ -645,6 +650,33 @@ __device__ __forceinline__ void seg_cost_p(double D, double V0, double A0, doubl
     const double G = Q4 * H4 + Q5 * H5 + Q6 * H6 + Q7 * H7;
     Qd = -(Q + 2.0 * G);
 }
+// Round 6: the same Q and Qd in the Legendre basis of the snap, from the scaled end data
+// directly (no P4..P7; used by the gradient passes, which need no coefficients).  The Gram
+// matrix above factors as H = L L^T with L^T E = diag(1, sqrt3, sqrt5, sqrt7) x an integer
+// map, so with
+//   g0 = j1 - j0,  g1 = 2 (A0 - A1) + (j0 + j1),  g2 = 12 (V1 - V0) - 6 (A0 + A1) + (j1 - j0),
+//   g3 = -120 D + 60 (V0 + V1) + 12 (A0 - A1) + (j0 + j1)
+// (the orthonormal shifted-Legendre coefficients of the snap, up to those square roots):
+//   Q = g0^2 + 3 g1^2 + 5 g2^2 + 7 g3^2,
+//   G = Qv^T H P = 3 g1 d1 + 5 g2 d2 + 7 g3 d3 with d the same map of (3D, 2V0, A0, 0, 2V1, A1, 0),
+//   Qd = -(Q + 2 G)
+// -- exact integer identities (checked symbolically), ~33 FP64 operations
+// per axis and segment instead of ~74 for P4..P7 + seg_cost_p.
+__device__ __forceinline__ void seg_grad_u(double D, double V0, double A0, double j0, double V1, double A1,
+                                           double j1, double& Q, double& Qd) {
+    const double sA = A0 - A1, pA = A0 + A1, sJ = j0 + j1, dJ = j1 - j0, sV = V0 + V1, dV = V1 - V0;
+    const double g0 = dJ;
+    const double g1 = fma(2.0, sA, sJ);
+    const double g2 = fma(12.0, dV, fma(-6.0, pA, dJ));
+    const double g3 = fma(-120.0, D, fma(60.0, sV, fma(12.0, sA, sJ)));
+    const double e1 = 6.0 * sA;                                     // 3 d1
+    const double e2 = fma(120.0, dV, -30.0 * pA);                   // 5 d2
+    const double e3 = fma(-2520.0, D, fma(840.0, sV, 84.0 * sA));   // 7 d3
+    Q = fma(g3, 7.0 * g3, fma(g2, 5.0 * g2, fma(g1, 3.0 * g1, g0 * g0)));
+    const double G = fma(g3, e3, fma(g2, e2, g1 * e1));
+    Qd = fma(-2.0, G, -Q);
+}
+
 // Q alone (the cost at the final times needs no derivative): 20 FP64 operations.
 __device__ __forceinline__ double seg_cost_q(double P4, double P5, double P6, double P7) {
     const double H4 = 576.0 * P4 + 1440.0 * P5 + 2880.0 * P6 + 5040.0 * P7;
@@ -704,6 +736,12 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
     const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
     const double D = (w1 - w0) * r3;
     const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
+#if TGMS_GRAD_LEGENDRE
+    if constexpr (is_grad<Out>::value) {
+        (void)r4;
+        double Q, Qd;
+        seg_grad_u(D, V0, A0, j0, V1, A1, j1, Q, Qd);
+#else
     const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
     const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
     const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
@@ -711,6 +749,7 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
     if constexpr (is_grad<Out>::value) {
         double Q, Qd;
         seg_cost_p(D, V0, A0, V1, A1, P4, P5, P6, P7, Q, Qd);
+#endif
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
         o.J += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
@@ -719,6 +758,13 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
         // knot data live for it) to the end of the solve
         asm volatile("" : "+v"(o.J), "+v"(o.dJ[e]));
     } else {
+#if TGMS_GRAD_LEGENDRE
+        const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
+        const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
+        const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
+        const double P7 =
+            -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+#endif
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
         for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
@@ -1530,11 +1576,12 @@ __device__ __forceinline__ void refine_update(const GradAcc<Chain<M>::NE>& G, bo
     }
     const double F = Fl + pair_swap(Fl);
     const bool ok = (st == TGMS_OK) && F > 0.0;
+    const double iF = 1.0 / F;  // one division per lane, not one per segment (round 6)
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         if (live && e < nmine) {
             const int phys = right ? M - 1 - e : e;
-            double dtau = -eta * Tl[e] * (G.dJ[e] + kT) / F;
+            double dtau = -eta * Tl[e] * (G.dJ[e] + kT) * iF;
             dtau = fmin(fmax(dtau, -0.5), 0.5);
             Tout[phys] = ok ? Tl[e] * exp(dtau) : Tl[e];
         }
@@ -1634,7 +1681,7 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
                                                      const int32_t* __restrict__ seg_offsets,
                                                      const double* __restrict__ W, const double* __restrict__ T,
                                                      const double* __restrict__ ED, double* __restrict__ C,
-                                                     int32_t* __restrict__ status) {
+                                                     int32_t* __restrict__ status, int32_t so_base = 0) {
     constexpr int NW = (M + 1) * 3;
     const int lane = threadIdx.x;
     const int slot = lane >> 1;
@@ -1650,7 +1697,7 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
     int32_t b = 0;
     if (live) {
         b = perm[i0 + slot];
-        const int64_t s0 = seg_offsets[b];
+        const int64_t s0 = (int64_t)seg_offsets[b] - so_base;  // (a slice of a larger batch's offsets)
         if (!right) sm.in.base[slot] = s0 * 24;
         const double* gW = W + (s0 + b) * 3;
         // the two lanes of a pair split the trajectory's rows
@@ -1741,13 +1788,14 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
             break;
         }
         const bool ok = (st == TGMS_OK) && F > 0.0;
+        const double iF = 1.0 / F;  // one division per lane and step, not one per segment (round 6)
         __syncthreads();  // every lane has read the stage before the times change
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             if (live && valid && e < nmine) {
                 const int phys = right ? M - 1 - e : e;
                 const double tl = Tl[e];
-                double dtau = -eta * tl * (G.dJ[e] + kT) / F;
+                double dtau = -eta * tl * (G.dJ[e] + kT) * iF;
                 dtau = fmin(fmax(dtau, -0.5), 0.5);
                 const double tn = ok ? tl * exp(dtau) : tl;
                 Tl[e] = tn;
@@ -1905,6 +1953,41 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_dev(const D
         if constexpr (mm >= MLO && mm <= MHI)                                                                 \
             refine_loop_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g],     \
                                           seg_offsets, W, T, ED, kT, eta, iters, cost, C, status, so_base);  \
+        break;
+        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
+        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
+        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
+        TGMS_MULTI_CASE(16)
+#undef TGMS_MULTI_CASE
+        default: break;
+    }
+}
+
+// The ragged solve with the device-computed plan (round 6: the pieces of a multi-GPU ragged
+// solve, and device 0's shard, are grouped on their device like the refinement loop's, so
+// the host makes no pass over the offsets): k_reduced_multi's blocks with the class table
+// read from device memory, grid dev_loop_grid(n), blocks past the last group return.
+template <int MLO, int MHI, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_reduced_multi_dev(const DevPlan* __restrict__ plan, int cls,
+                                                                            const int32_t* __restrict__ seg_offsets,
+                                                                            const double* __restrict__ W,
+                                                                            const double* __restrict__ T,
+                                                                            const double* __restrict__ ED,
+                                                                            double* __restrict__ C,
+                                                                            int32_t* __restrict__ status) {
+    __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
+    const GroupTable& tab = plan->tab[cls];
+    const int ng = tab.ngroups;
+    if (ng <= 0 || (int64_t)blockIdx.x >= tab.blk_end[ng - 1]) return;
+    int64_t blk;
+    const int g = group_of(tab, blockIdx.x, blk);
+    const int32_t so_base = plan->so_base;
+    switch (tab.m[g]) {
+#define TGMS_MULTI_CASE(mm)                                                                                 \
+    case mm:                                                                                               \
+        if constexpr (mm >= MLO && mm <= MHI)                                                              \
+            reduced_ragged_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g], \
+                                             seg_offsets, W, T, ED, C, status, so_base);                  \
         break;
         TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
         TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
@@ -2957,6 +3040,28 @@ hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const
     }
     if (cls == 0) return loop_dev_launch<1, A, false>(0, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
     return loop_dev_launch<A + 1, 16, false>(1, n, plan, so, W, T, ED, kT, eta, iters, cost, C, status, stream);
+}
+
+template <int MLO, int MHI, bool HAS_ED>
+hipError_t solve_dev_launch(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+                            const double* T, const double* ED, double* C, int32_t* status, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if constexpr (MLO <= MHI)
+        TGMS_LAUNCH((k_reduced_multi_dev<MLO, MHI, HAS_ED>), dim3(dev_loop_grid(n)), dim3(W64), 0, stream, plan, cls,
+                    so, W, T, ED, C, status);
+    return hipSuccess;
+}
+
+hipError_t launch_reduced_multi_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+                                    const double* T, const double* ED, double* C, int32_t* status,
+                                    hipStream_t stream) {
+    constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
+    if (ED) {
+        if (cls == 0) return solve_dev_launch<1, E, true>(0, n, plan, so, W, T, ED, C, status, stream);
+        return solve_dev_launch<E + 1, 16, true>(1, n, plan, so, W, T, ED, C, status, stream);
+    }
+    if (cls == 0) return solve_dev_launch<1, A, false>(0, n, plan, so, W, T, ED, C, status, stream);
+    return solve_dev_launch<A + 1, 16, false>(1, n, plan, so, W, T, ED, C, status, stream);
 }
 
 hipError_t launch_ragged_multi(int cls, const GroupTable& tab, bool refine, const int32_t* so, const double* W,
