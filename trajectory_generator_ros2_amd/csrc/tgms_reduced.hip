@@ -726,6 +726,26 @@ template <int M, class Out>
 __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, double r, bool right, int e, int a,
                                             const double (&xs)[3], const double (&xe)[3], bool has_r,
                                             bool zero = false) {
+#if TGMS_GRAD_LEGENDRE
+    if constexpr (is_grad<Out>::value) {
+        // The snap cost of a segment and its T-derivative do not change under time reversal
+        // (the odd lane's virtual segment is the physical one run backwards, with
+        // (D, v, a, j) -> (-D, -v, a, -j) and the ends swapped: g0, g2, d2 keep their sign,
+        // g1, g3, d1, d3 flip, and only squares and products of equal parity enter Q and G),
+        // so the gradient pass takes the virtual end data as they are: no frame selects.
+        const double r2 = r * r, r3 = r2 * r;
+        double Q, Qd;
+        seg_grad_u((we - ws) * r3, xs[0] * r2, xs[1] * r, xs[2], xe[0] * r2, xe[1] * r, xe[2], Q, Qd);
+        const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
+        o.J += mine ? r * Q : 0.0;
+        o.dJ[e] += mine ? r2 * Qd : 0.0;
+        // anchored here: nothing stores these sums until the step's update, so without
+        // the anchor the compiler sinks every segment's cost arithmetic (and keeps all
+        // knot data live for it) to the end of the solve
+        asm volatile("" : "+v"(o.J), "+v"(o.dJ[e]));
+        return;
+    }
+#endif
     const double w0 = right ? we : ws, w1 = right ? ws : we;
     // the odd lane runs the segment backwards: physical start = virtual knot e+1, with P
     const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
@@ -736,20 +756,14 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
     const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
     const double D = (w1 - w0) * r3;
     const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
-#if TGMS_GRAD_LEGENDRE
-    if constexpr (is_grad<Out>::value) {
-        (void)r4;
-        double Q, Qd;
-        seg_grad_u(D, V0, A0, j0, V1, A1, j1, Q, Qd);
-#else
     const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
     const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
     const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
     const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
-    if constexpr (is_grad<Out>::value) {
+#if !TGMS_GRAD_LEGENDRE
+    if constexpr (is_grad<Out>::value) {  // round 5's form (A/B builds)
         double Q, Qd;
         seg_cost_p(D, V0, A0, V1, A1, P4, P5, P6, P7, Q, Qd);
-#endif
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
         o.J += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
@@ -757,14 +771,10 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
         // the anchor the compiler sinks every segment's cost arithmetic (and keeps all
         // knot data live for it) to the end of the solve
         asm volatile("" : "+v"(o.J), "+v"(o.dJ[e]));
-    } else {
-#if TGMS_GRAD_LEGENDRE
-        const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
-        const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
-        const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
-        const double P7 =
-            -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+        return;
+    }
 #endif
+    if constexpr (!is_grad<Out>::value) {
         double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
         for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
