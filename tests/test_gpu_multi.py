@@ -239,7 +239,7 @@ def test_multi_error_path_leaves_handle_usable(solver, hook):
 def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
     """Round 5: tgms_refine_loop_multi_device does no pass over the offsets on the host; a
     trajectory with M outside 1..16 strictly inside a piece fails that piece on its device
-    (k_group_plan): the call returns OK, the bad trajectory's status is TGMS_ERR_INVALID_ARG
+    (k_plan_scatter): the call returns OK, the bad trajectory's status is TGMS_ERR_INVALID_ARG
     and the rest of its piece TGMS_ERR_SKIPPED (round 6, ADVICE r05: the valid trajectories
     of a failed piece are told apart from the bad one), all with zero coefficients and costs
     and the times kept, every other piece refines normally.  The
@@ -284,7 +284,7 @@ def test_refine_multi_bad_offsets_fail_on_the_device(multi, request):
 def test_solve_multi_ragged_bad_offsets_fail_on_the_device(multi, request):
     """Round 6: a ragged reduced solve over the multi-GPU path no longer
     scans the offsets on the host -- each piece (and device 0's shard) is grouped on its
-    device (k_perm_hist -> k_group_plan -> k_perm_scatter_dev -> k_reduced_multi_dev).  A
+    device (k_perm_hist -> k_plan_scatter -> k_reduced_multi_dev).  A
     trajectory with M outside 1..16 strictly inside the batch: the call returns OK, that
     trajectory reads TGMS_ERR_INVALID_ARG, the rest of its piece (or of device 0's shard)
     TGMS_ERR_SKIPPED, all with zero coefficients; every other trajectory equals the

@@ -216,7 +216,7 @@ def test_schedule_arguments(lib):
 
 def test_refine_schedule_leaves_per_trajectory_checks_to_the_devices(lib):
     """Round 5: the refinement loop's host work reads only the cuts.  A bad M strictly
-    inside a piece passes the host (its device's k_group_plan rejects that piece:
+    inside a piece passes the host (its device's k_plan_scatter rejects that piece:
     tests/test_gpu_multi.py::test_refine_multi_bad_offsets_fail_on_the_device); offsets
     whose shard or piece spans no M in 1..16 can give (the workspaces are sized from them) are
     refused; a decrease that the cuts do not expose is again the devices' to reject."""

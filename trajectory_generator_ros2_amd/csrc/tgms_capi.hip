@@ -599,7 +599,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, int64_t S, con
         // occupancy class runs its whole loop (steps, cost, final solve) in ONE launch,
         // times kept in LDS between steps and updated in place in T[0]; the two classes'
         // launches run side by side.  The grouping by M and both classes' tables are
-        // computed on the device first (k_perm_hist, k_group_plan, k_perm_scatter_dev).
+        // computed on the device first (k_perm_hist, k_plan_scatter).
         if (!dp || !dp->hist || !dp->perm || !dp->plan)
             return set_err(h, TGMS_ERR_DEVICE, "internal: ragged refinement loop without plan buffers");
         TGMS_HIP(h, tgms::launch_group_plan_dev(B, S, d_so, ED != nullptr, dp->hist, dp->perm, dp->plan, st, C, cost,
@@ -634,7 +634,7 @@ tgms_status refine_loop(tgms_handle* h, const Plan& p, int32_t B, int64_t S, con
 }
 
 // A ragged solve (reduced method) grouped on the device (round 6): k_perm_hist ->
-// k_group_plan -> k_perm_scatter_dev, then both occupancy classes from the device plan, so
+// k_plan_scatter, then both occupancy classes from the device plan, so
 // the host makes no pass over the offsets.  A bad M fails the batch on the device
 // (TGMS_ERR_INVALID_ARG where M is outside 1..16, TGMS_ERR_SKIPPED elsewhere, zeros).
 tgms_status solve_ragged_dev(tgms_handle* h, int32_t B, int64_t S, const int32_t* d_so, const double* W,
@@ -1939,7 +1939,7 @@ tgms_status tgms_refine_loop_multi_device(tgms_handle* h, int32_t B, const int32
     // No pass over the offsets on the host (round 5, VERDICT r04 item 2: the host work before
     // the first transfer stays O(devices x pieces x log B)).  The host checks what its schedule
     // rests on -- so[0], the span, the shard and piece cuts (multi_enqueue) -- and every
-    // piece's device plan checks each trajectory's M (k_group_plan: a piece whose offsets are
+    // piece's device plan checks each trajectory's M (k_plan_scatter: a piece whose offsets are
     // bad runs nothing and returns TGMS_ERR_INVALID_ARG statuses and zeros).  Every batch,
     // uniform ones too, runs the device-grouped loop.
     if (B < 0) return set_err(h, TGMS_ERR_INVALID_ARG, "B < 0");

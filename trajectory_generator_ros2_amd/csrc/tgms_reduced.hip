@@ -1937,7 +1937,7 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_multi(GroupTable
     }
 }
 
-// The refinement loop with the device-computed plan (k_group_plan): the class's group
+// The refinement loop with the device-computed plan (k_plan_scatter): the class's group
 // table is read from device memory (scalar loads), the grid covers every wavefront a
 // table can hold (dev_loop_grid) and the blocks past the class's last group return.
 template <int MLO, int MHI, bool HAS_ED>
@@ -2084,86 +2084,110 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const in
     perm_scatter_body(B, so, hist, [&](int g) { return st.s[g]; }, perm);
 }
 
-__global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter_dev(int32_t B, const int32_t* __restrict__ so,
-                                                                 const int32_t* __restrict__ hist,
-                                                                 const DevPlan* __restrict__ plan,
-                                                                 int32_t* __restrict__ perm) {
-    if (plan->bad) return;
-    perm_scatter_body(B, so, hist, [&](int g) { return plan->starts[g]; }, perm);
-}
-
-// The device-side plan (DevPlan, tgms_internal.h) from k_perm_hist's block counts: one
-// workgroup sums them per M (16 bins x 64 strided partial sums), checks the offsets against
-// the host's B and S, and thread 0 lays out the starts and both classes' group tables in
-// the order the host planner used (M descending within a class).  A bad plan runs nothing
-// and marks the trajectories whose own M is outside 1..16 TGMS_ERR_INVALID_ARG and the
-// others TGMS_ERR_SKIPPED, all outputs exact zeros (rare path: one workgroup clears the
-// S x 24 coefficients).
-constexpr int PLAN_THREADS = 1024;
-__global__ __launch_bounds__(PLAN_THREADS) void k_group_plan(int32_t n, int64_t S, const int32_t* __restrict__ so,
-                                                            int has_ed, const int32_t* __restrict__ hist,
-                                                            int32_t* __restrict__ perm, DevPlan* __restrict__ plan,
-                                                            int32_t* __restrict__ status, double* __restrict__ C,
-                                                            double* __restrict__ cost) {
-    constexpr int NPART = PLAN_THREADS / 16;
-    __shared__ int32_t part[NPART][PERM_BINS];
-    __shared__ int32_t cnt[PERM_BINS];
+// The device-side plan (DevPlan, tgms_internal.h) and the scatter in ONE launch after
+// k_perm_hist (round 6: a one-workgroup planning kernel between the two cost a launch, ~6 us
+// of a 0.39 ms config-5 call).  Every block sums the per-block counts itself, one wave per
+// group M: over the blocks before it (its scatter base) and over all blocks (the totals, so
+// the starts); it checks the offsets against the host's B and S; block 0 also writes the
+// plan the class loops read (so_base, starts and both classes' group tables in the order the
+// host planner used, M descending within a class).  A bad plan scatters nothing and marks
+// the trajectories whose own M is outside 1..16 TGMS_ERR_INVALID_ARG and the others
+// TGMS_ERR_SKIPPED, all outputs exact zeros (each block its own trajectories and its share
+// of the S x 24 coefficients).
+__global__ __launch_bounds__(PERM_BLOCK) void k_plan_scatter(int32_t n, int64_t S, const int32_t* __restrict__ so,
+                                                             int has_ed, const int32_t* __restrict__ hist,
+                                                             int32_t* __restrict__ perm, DevPlan* __restrict__ plan,
+                                                             int32_t* __restrict__ status, double* __restrict__ C,
+                                                             double* __restrict__ cost) {
+    __shared__ int32_t wc[PERM_BLOCK / W64][PERM_BINS];
+    __shared__ int32_t before[PERM_BINS], cnt[PERM_BINS], base[PERM_BINS];
     __shared__ int32_t bad_s;
-    const int t = threadIdx.x;
-    const int nblk = (n + PERM_BLOCK - 1) / PERM_BLOCK;
-    {
-        const int bin = (t & 15) + 1, j0 = t >> 4;
-        int32_t s = 0;
-        for (int v = j0; v < nblk; v += NPART) s += hist[(int64_t)v * PERM_BINS + bin];
-        part[j0][bin] = s;
+    const int t = threadIdx.x, w = t / W64, l = t % W64;
+    const int nblk = (int)gridDim.x;
+    const int64_t b = (int64_t)blockIdx.x * PERM_BLOCK + t;
+    const int m = perm_m(so, b, n);
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int k = 1; k < PERM_BINS; ++k) {
+        const unsigned long long mask = __ballot(m == k);
+        if (m == k) mine = mask;
+        if (l == 0) wc[w][k] = __popcll(mask);
     }
-    __syncthreads();
-    if (t < 16) {
-        int32_t c = 0;
-        for (int j = 0; j < NPART; ++j) c += part[j][t + 1];
-        cnt[t + 1] = c;
+    {  // PERM_BLOCK / W64 == PERM_BINS - 1 waves: wave w sums group w + 1 over the blocks
+        const int g = w + 1;
+        int32_t sb = 0, sa = 0;
+        for (int v = l; v < nblk; v += W64) {
+            const int32_t c = hist[(int64_t)v * PERM_BINS + g];
+            sa += c;
+            sb += (v < (int)blockIdx.x) ? c : 0;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sa += __shfl_xor(sa, off);
+            sb += __shfl_xor(sb, off);
+        }
+        if (l == 0) {
+            before[g] = sb;
+            cnt[g] = sa;
+        }
     }
     __syncthreads();
     if (t == 0) {
         int64_t tot = 0;
-        for (int m = 1; m < PERM_BINS; ++m) tot += cnt[m];
+        for (int k = 1; k < PERM_BINS; ++k) tot += cnt[k];
         const int32_t so0 = so[0];
         const bool bad = tot != n || (int64_t)so[n] - so0 != S;
-        plan->so_base = so0;
-        plan->bad = bad ? 1 : 0;
         bad_s = bad ? 1 : 0;
-        const int max2 = has_ed ? TGMS_TWO_WAVE_MAX_M_ED : TGMS_TWO_WAVE_MAX_M;
+        int32_t starts[PERM_BINS];
         int32_t st = 0;
-        plan->starts[0] = 0;
-        for (int m = 1; m < PERM_BINS; ++m) {
-            plan->starts[m] = st;
-            st += bad ? 0 : cnt[m];
+        starts[0] = 0;
+        for (int k = 1; k < PERM_BINS; ++k) {
+            starts[k] = st;
+            base[k] = st + before[k];
+            st += bad ? 0 : cnt[k];
         }
-        int ng[2] = {0, 0};
-        int32_t be[2] = {0, 0};
-        for (int m = PERM_BINS - 1; m >= 1; --m) {
-            if (bad || !cnt[m]) continue;
-            const int c = m > max2 ? 1 : 0;
-            GroupTable& tb = plan->tab[c];
-            const int g = ng[c]++;
-            be[c] += (cnt[m] + RAGGED_TPW - 1) / RAGGED_TPW;
-            tb.m[g] = m;
-            tb.n[g] = cnt[m];
-            tb.perm[g] = perm + plan->starts[m];
-            tb.blk_end[g] = be[c];
+        if (blockIdx.x == 0) {
+            plan->so_base = so0;
+            plan->bad = bad ? 1 : 0;
+            for (int k = 0; k < PERM_BINS; ++k) plan->starts[k] = starts[k];
+            const int max2 = has_ed ? TGMS_TWO_WAVE_MAX_M_ED : TGMS_TWO_WAVE_MAX_M;
+            int ng[2] = {0, 0};
+            int32_t be[2] = {0, 0};
+            for (int k = PERM_BINS - 1; k >= 1; --k) {
+                if (bad || !cnt[k]) continue;
+                const int c = k > max2 ? 1 : 0;
+                GroupTable& tb = plan->tab[c];
+                const int g = ng[c]++;
+                be[c] += (cnt[k] + RAGGED_TPW - 1) / RAGGED_TPW;
+                tb.m[g] = k;
+                tb.n[g] = cnt[k];
+                tb.perm[g] = perm + starts[k];
+                tb.blk_end[g] = be[c];
+            }
+            plan->tab[0].ngroups = ng[0];
+            plan->tab[1].ngroups = ng[1];
         }
-        plan->tab[0].ngroups = ng[0];
-        plan->tab[1].ngroups = ng[1];
     }
     __syncthreads();
-    if (!bad_s) return;
-    for (int64_t b = t; b < n; b += PLAN_THREADS) {
-        const int64_t m = (int64_t)so[b + 1] - so[b];
-        if (status) status[b] = (m < 1 || m > TGMS_MAX_SEGMENTS) ? TGMS_ERR_INVALID_ARG : TGMS_ERR_SKIPPED;
-        if (cost) cost[b] = 0.0;
+    if (bad_s) {
+        if (b < n) {
+            const int64_t mb = (int64_t)so[b + 1] - so[b];
+            if (status) status[b] = (mb < 1 || mb > TGMS_MAX_SEGMENTS) ? TGMS_ERR_INVALID_ARG : TGMS_ERR_SKIPPED;
+            if (cost) cost[b] = 0.0;
+        }
+        if (C) {
+            const int64_t total = S * 24, chunk = (total + nblk - 1) / nblk;
+            const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = i0 + chunk < total ? i0 + chunk : total;
+            for (int64_t i = i0 + t; i < i1; i += PERM_BLOCK) C[i] = 0.0;
+        }
+        return;
     }
-    if (C)
-        for (int64_t i = t; i < S * 24; i += PLAN_THREADS) C[i] = 0.0;
+    if (m >= 1 && m < PERM_BINS) {  // (a device copy of the offsets that disagrees with the
+        int32_t r = base[m];         // host's must not write out of range)
+        for (int v = 0; v < w; ++v) r += wc[v][m];
+        r += __popcll(mine & ((1ull << l) - 1ull));
+        if (r >= 0 && r < n) perm[r] = (int32_t)b;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -3021,9 +3045,8 @@ hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int ha
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + PERM_BLOCK - 1) / PERM_BLOCK);
     TGMS_LAUNCH(k_perm_hist, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, so, hist);
-    TGMS_LAUNCH(k_group_plan, dim3(1), dim3(PLAN_THREADS), 0, stream, n, S, so, has_ed, hist, perm, plan, status, C,
-                cost);
-    TGMS_LAUNCH(k_perm_scatter_dev, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, so, hist, plan, perm);
+    TGMS_LAUNCH(k_plan_scatter, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, S, so, has_ed, hist, perm, plan, status,
+                C, cost);
     return hipSuccess;
 }
 
