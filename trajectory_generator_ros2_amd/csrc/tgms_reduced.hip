@@ -378,6 +378,36 @@ __device__ __forceinline__ int out_step(const OutCtx&, int e) { return e; }
 // ---------------------------------------------------------------------------
 // Block algebra.
 
+// ---------------------------------------------------------------------------
+// The lane-pair kernels solve the reduced system in scaled knot unknowns x' = S^-1 x,
+// S = diag(21, 3, 1) on (v, a, j) (round 6): every block becomes S H S.  KSE factors as
+// a_d b_e c_(d+e) with a = (1, 1, 3/7), b = (1, -1, 3/7), so the scaled coupling
+// S C_i S is the signed Hankel matrix [sigma_e q_(d+e)], sigma = (+, -, +), of the five
+// numbers q_k = HNK_k r_i^(5-k): 5 multiplies per coupling instead of 9 (the signs fold into
+// the consuming FMAs), integer constants throughout.  Factorisation, substitutions and the
+// interface keep their form; the emission and the gradient fold 21 and 3 into their
+// constants, and the given end derivatives are scaled once on load.  TGMS_PAIR_SCALED=0
+// solves the unscaled system (A/B builds).  The lane kernel (k_lane_uniform) is unscaled.
+#ifndef TGMS_PAIR_SCALED
+#define TGMS_PAIR_SCALED 1
+#endif
+#if TGMS_PAIR_SCALED
+constexpr double PSV = 21.0, PSA = 3.0;  // v = 21 v', a = 3 a', j = j'
+__device__ constexpr double pKSS[3][3] = {{11430720, 340200, 10080}, {340200, 10800, 360}, {10080, 360, 16}};
+__device__ constexpr double pKEE[3][3] = {{11430720, -340200, 10080}, {-340200, 10800, -360}, {10080, -360, 16}};
+__device__ constexpr double pKSE[3][3] = {{10795680, -294840, 7560}, {294840, -7560, 180}, {7560, -180, 4}};
+__device__ constexpr double pKSP[3] = {-1058400, -30240, -840};
+__device__ constexpr double pKEP[3] = {-1058400, 30240, -840};
+#else
+constexpr double PSV = 1.0, PSA = 1.0;
+__device__ constexpr double pKSS[3][3] = {{25920, 5400, 480}, {5400, 1200, 120}, {480, 120, 16}};
+__device__ constexpr double pKEE[3][3] = {{25920, -5400, 480}, {-5400, 1200, -120}, {480, -120, 16}};
+__device__ constexpr double pKSE[3][3] = {{24480, -4680, 360}, {4680, -840, 60}, {360, -60, 4}};
+__device__ constexpr double pKSP[3] = {-50400, -10080, -840};
+__device__ constexpr double pKEP[3] = {-50400, 10080, -840};
+#endif
+constexpr double PSI[3] = {1.0 / PSV, 1.0 / PSA, 1.0};  // x' = x * PSI (end derivatives on load)
+
 struct Sym3 {  // symmetric 3x3 block (upper triangle)
     double a00, a01, a02, a11, a12, a22;
 };
@@ -425,8 +455,8 @@ __device__ __forceinline__ Sym3 knot_diag(const double (&pp)[8], const double (&
 template <bool HAS_ED>
 __device__ __forceinline__ void knot_rhs(const LaneView& L, int k, const double (&pp)[8], const double (&pn)[8],
                                          const double (&u0)[3][3], double (&y)[3][3]) {
-    const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
-    const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+    const double fp[3] = {-pKEP[0] * pp[6], -pKEP[1] * pp[5], -pKEP[2] * pp[4]};
+    const double fn[3] = {-pKSP[0] * pn[6], -pKSP[1] * pn[5], -pKSP[2] * pn[4]};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const double wk = L.w(k, a);
@@ -440,7 +470,7 @@ __device__ __forceinline__ void knot_rhs(const LaneView& L, int k, const double 
         for (int d = 0; d < 3; ++d)
 #pragma unroll
             for (int e = 0; e < 3; ++e) {
-                const double c0 = KSE[e][d] * pp[5 - d - e];
+                const double c0 = pKSE[e][d] * pp[5 - d - e];
 #pragma unroll
                 for (int a = 0; a < 3; ++a) y[d][a] -= c0 * u0[e][a];
             }
@@ -453,6 +483,35 @@ __device__ __forceinline__ void coupling(const double (&p)[8], double (&B)[3][3]
     for (int d = 0; d < 3; ++d)
 #pragma unroll
         for (int e = 0; e < 3; ++e) B[d][e] = KSE[d][e] * p[5 - d - e];
+}
+
+__device__ __forceinline__ Sym3 knot_diag_p(const double (&pp)[8], const double (&pn)[8]) {
+    Sym3 D;
+    D.a00 = pKEE[0][0] * pp[5] + pKSS[0][0] * pn[5];
+    D.a01 = pKEE[0][1] * pp[4] + pKSS[0][1] * pn[4];
+    D.a02 = pKEE[0][2] * pp[3] + pKSS[0][2] * pn[3];
+    D.a11 = pKEE[1][1] * pp[3] + pKSS[1][1] * pn[3];
+    D.a12 = pKEE[1][2] * pp[2] + pKSS[1][2] * pn[2];
+    D.a22 = pKEE[2][2] * pp[1] + pKSS[2][2] * pn[1];
+    return D;
+}
+
+__device__ __forceinline__ void coupling_p(const double (&p)[8], double (&B)[3][3]) {
+#if TGMS_PAIR_SCALED
+    const double q0 = 10795680.0 * p[5], q1 = 294840.0 * p[4], q2 = 7560.0 * p[3], q3 = 180.0 * p[2];
+    const double q4 = 4.0 * p[1];
+    B[0][0] = q0;
+    B[0][1] = -q1;
+    B[0][2] = q2;
+    B[1][0] = q1;
+    B[1][1] = -q2;
+    B[1][2] = q3;
+    B[2][0] = q2;
+    B[2][1] = -q3;
+    B[2][2] = q4;
+#else
+    coupling(p, B);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -498,10 +557,10 @@ __device__ __forceinline__ void ax_factor(AxFactors<M>& Fa, const LaneView& L, b
         const int k = s + 1;
         double pn[8];
         rpowers(L.r(k), pn);
-        Sym3 D = knot_diag(pp, pn);
+        Sym3 D = knot_diag_p(pp, pn);
         if (s >= 1) {
             double B[3][3], Wc[3][3];
-            coupling(pp, B);  // H_{k-1, k}
+            coupling_p(pp, B);  // H_{k-1, k}
 #pragma unroll
             for (int e = 0; e < 3; ++e)
                 ldl3_solve(Fa.F[s - 1], B[0][e], B[1][e], B[2][e], Wc[0][e], Wc[1][e], Wc[2][e]);
@@ -535,7 +594,7 @@ __device__ __forceinline__ void ax_factor(AxFactors<M>& Fa, const LaneView& L, b
     {
         double pc[8];
         rpowers(L.r(nl), pc);  // physical segment c = virtual segment nl on both lanes
-        coupling(pc, Fa.Cc);
+        coupling_p(pc, Fa.Cc);
     }
     bool ok1, ok2;
     Fa.FR = ldl3s(DR, ok1);
@@ -560,8 +619,8 @@ __device__ __forceinline__ void ax_factor(AxFactors<M>& Fa, const LaneView& L, b
 template <bool HAS_ED>
 __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, const double (&pp)[8],
                                               const double (&pn)[8], const double (&u0)[3], double (&y)[3]) {
-    const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
-    const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+    const double fp[3] = {-pKEP[0] * pp[6], -pKEP[1] * pp[5], -pKEP[2] * pp[4]};
+    const double fn[3] = {-pKSP[0] * pn[6], -pKSP[1] * pn[5], -pKSP[2] * pn[4]};
     const double wk = L.w(k, a);
     const double dp = wk - L.w(k - 1, a);
     const double dn = L.w(k + 1, a) - wk;
@@ -571,7 +630,7 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
 #pragma unroll
         for (int d = 0; d < 3; ++d)
 #pragma unroll
-            for (int e = 0; e < 3; ++e) y[d] -= (KSE[e][d] * pp[5 - d - e]) * u0[e];
+            for (int e = 0; e < 3; ++e) y[d] -= (pKSE[e][d] * pp[5 - d - e]) * u0[e];
     }
 }
 
@@ -579,8 +638,8 @@ __device__ __forceinline__ void knot_rhs_axis(const LaneView& L, int k, int a, c
 template <bool HAS_ED>
 __device__ __forceinline__ void knot_rhs_vals(int k, double wm, double wk, double wn, const double (&pp)[8],
                                               const double (&pn)[8], const double (&u0)[3], double (&y)[3]) {
-    const double fp[3] = {-KEP[0] * pp[6], -KEP[1] * pp[5], -KEP[2] * pp[4]};
-    const double fn[3] = {-KSP[0] * pn[6], -KSP[1] * pn[5], -KSP[2] * pn[4]};
+    const double fp[3] = {-pKEP[0] * pp[6], -pKEP[1] * pp[5], -pKEP[2] * pp[4]};
+    const double fn[3] = {-pKSP[0] * pn[6], -pKSP[1] * pn[5], -pKSP[2] * pn[4]};
     const double dp = wk - wm;
     const double dn = wn - wk;
 #pragma unroll
@@ -589,7 +648,7 @@ __device__ __forceinline__ void knot_rhs_vals(int k, double wm, double wk, doubl
 #pragma unroll
         for (int d = 0; d < 3; ++d)
 #pragma unroll
-            for (int e = 0; e < 3; ++e) y[d] -= (KSE[e][d] * pp[5 - d - e]) * u0[e];
+            for (int e = 0; e < 3; ++e) y[d] -= (pKSE[e][d] * pp[5 - d - e]) * u0[e];
     }
 }
 
@@ -661,17 +720,18 @@ __device__ __forceinline__ void seg_cost_p(double D, double V0, double A0, doubl
 //   G = Qv^T H P = 3 g1 d1 + 5 g2 d2 + 7 g3 d3 with d the same map of (3D, 2V0, A0, 0, 2V1, A1, 0),
 //   Qd = -(Q + 2 G)
 // -- exact integer identities (checked symbolically), ~33 FP64 operations
-// per axis and segment instead of ~74 for P4..P7 + seg_cost_p.
+// per axis and segment instead of ~74 for P4..P7 + seg_cost_p.  V and A arrive in the pair
+// kernels' scaled unknowns (V = PSV V', A = PSA A'); the factors fold into the constants.
 __device__ __forceinline__ void seg_grad_u(double D, double V0, double A0, double j0, double V1, double A1,
                                            double j1, double& Q, double& Qd) {
     const double sA = A0 - A1, pA = A0 + A1, sJ = j0 + j1, dJ = j1 - j0, sV = V0 + V1, dV = V1 - V0;
     const double g0 = dJ;
-    const double g1 = fma(2.0, sA, sJ);
-    const double g2 = fma(12.0, dV, fma(-6.0, pA, dJ));
-    const double g3 = fma(-120.0, D, fma(60.0, sV, fma(12.0, sA, sJ)));
-    const double e1 = 6.0 * sA;                                     // 3 d1
-    const double e2 = fma(120.0, dV, -30.0 * pA);                   // 5 d2
-    const double e3 = fma(-2520.0, D, fma(840.0, sV, 84.0 * sA));   // 7 d3
+    const double g1 = fma(2.0 * PSA, sA, sJ);
+    const double g2 = fma(12.0 * PSV, dV, fma(-6.0 * PSA, pA, dJ));
+    const double g3 = fma(-120.0, D, fma(60.0 * PSV, sV, fma(12.0 * PSA, sA, sJ)));
+    const double e1 = (6.0 * PSA) * sA;                                              // 3 d1
+    const double e2 = fma(120.0 * PSV, dV, (-30.0 * PSA) * pA);                      // 5 d2
+    const double e3 = fma(-2520.0, D, fma(840.0 * PSV, sV, (84.0 * PSA) * sA));      // 7 d3
     Q = fma(g3, 7.0 * g3, fma(g2, 5.0 * g2, fma(g1, 3.0 * g1, g0 * g0)));
     const double G = fma(g3, e3, fma(g2, e2, g1 * e1));
     Qd = fma(-2.0, G, -Q);
@@ -684,32 +744,6 @@ __device__ __forceinline__ double seg_cost_q(double P4, double P5, double P6, do
     const double H6 = 2880.0 * P4 + 10800.0 * P5 + 25920.0 * P6 + 50400.0 * P7;
     const double H7 = 5040.0 * P4 + 20160.0 * P5 + 50400.0 * P6 + 100800.0 * P7;
     return P4 * H4 + P5 * H5 + P6 * H6 + P7 * H7;
-}
-
-// Coefficients of axis a of virtual segment e (virtual knots e, e+1 with derivatives
-// xs, xe of that axis), physical order c0..c7.
-__device__ __forceinline__ void row_coeffs(const LaneView& L, bool right, int e, int a, const double (&xs)[3],
-                                           const double (&xe)[3], double (&c)[8]) {
-    const double ws = L.w(e, a), we = L.w(e + 1, a);
-    const double w0 = right ? we : ws, w1 = right ? ws : we;
-    const double v0 = right ? -xe[0] : xs[0], a0 = right ? xe[1] : xs[1], j0 = right ? -xe[2] : xs[2];
-    const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
-    const double r = L.r(e);
-    const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
-    const double D = (w1 - w0) * r3;
-    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
-    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
-    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
-    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
-    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
-    c[0] = w0;
-    c[1] = v0;
-    c[2] = 0.5 * a0;
-    c[3] = j0 * (1.0 / 6.0);
-    c[4] = P4 * r;
-    c[5] = P5 * r2;
-    c[6] = P6 * r3;
-    c[7] = P7 * r4;
 }
 
 // Where one axis of segment e goes, per output kind.
@@ -755,15 +789,19 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
     //   D = (w1 - w0) r^3, V = v r^2, A = a r, J = j at both ends.
     const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
     const double D = (w1 - w0) * r3;
-    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
-    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
-    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
-    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
-    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;  // scaled: x PSV, x PSA
+    const double P4 = 35.0 * D - (20.0 * PSV) * V0 - (5.0 * PSA) * A0 - (2.0 / 3.0) * j0 - (15.0 * PSV) * V1 +
+                      (2.5 * PSA) * A1 - (1.0 / 6.0) * j1;
+    const double P5 = -84.0 * D + (45.0 * PSV) * V0 + (10.0 * PSA) * A0 + j0 + (39.0 * PSV) * V1 -
+                      (7.0 * PSA) * A1 + 0.5 * j1;
+    const double P6 = 70.0 * D - (36.0 * PSV) * V0 - (7.5 * PSA) * A0 - (2.0 / 3.0) * j0 - (34.0 * PSV) * V1 +
+                      (6.5 * PSA) * A1 - 0.5 * j1;
+    const double P7 = -20.0 * D + (10.0 * PSV) * V0 + (2.0 * PSA) * A0 + (1.0 / 6.0) * j0 + (10.0 * PSV) * V1 -
+                      (2.0 * PSA) * A1 + (1.0 / 6.0) * j1;
 #if !TGMS_GRAD_LEGENDRE
     if constexpr (is_grad<Out>::value) {  // round 5's form (A/B builds)
         double Q, Qd;
-        seg_cost_p(D, V0, A0, V1, A1, P4, P5, P6, P7, Q, Qd);
+        seg_cost_p(D, PSV * V0, PSA * A0, PSV * V1, PSA * A1, P4, P5, P6, P7, Q, Qd);
         const bool mine = has_r || !right;  // the odd lane's last step may duplicate the even lane's
         o.J += mine ? r * Q : 0.0;
         o.dJ[e] += mine ? r2 * Qd : 0.0;
@@ -775,7 +813,7 @@ __device__ __forceinline__ void emit_axis_v(const Out& o, double ws, double we, 
     }
 #endif
     if constexpr (!is_grad<Out>::value) {
-        double c[8] = {w0, v0, 0.5 * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
+        double c[8] = {w0, PSV * v0, (0.5 * PSA) * a0, j0 * (1.0 / 6.0), P4 * r, P5 * r2, P6 * r3, P7 * r4};
 #pragma unroll
         for (int j = 0; j < 8; ++j) c[j] = zero ? 0.0 : c[j];  // a failed factorisation: exact zeros
         if constexpr (is_cost_out<Out>::value) {
@@ -828,7 +866,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
         for (int d = 0; d < 3; ++d) {
             const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
             const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
-            u0[d] = right ? ((d == 1) ? s1 : -s1) : s0;
+            u0[d] = (right ? ((d == 1) ? s1 : -s1) : s0) * PSI[d];  // scaled unknowns
         }
         // ---- forward substitution ----
         MARK(ax_fwd);
@@ -860,7 +898,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #endif
                 if (s >= 1) {
                     double B[3][3], v0, v1, v2;
-                    coupling(pp, B);
+                    coupling_p(pp, B);
                     ldl3_solve(Fa.F[s - 1], Y[s - 1][0], Y[s - 1][1], Y[s - 1][2], v0, v1, v2);
 #pragma unroll
                     for (int d = 0; d < 3; ++d) y[d] -= B[0][d] * v0 + B[1][d] * v1 + B[2][d] * v2;
@@ -888,7 +926,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
             {
                 double pc[8];
                 rpowers(L.r(nl), pc);
-                coupling(pc, Cc);
+                coupling_p(pc, Cc);
             }
             double g0, g1, g2;
             ldl3_solve(Fa.FR, yR[0], yR[1], yR[2], g0, g1, g2);
@@ -942,7 +980,7 @@ __device__ __forceinline__ int32_t pair_solve_ax(const LaneView& L, bool right, 
 #else
                     rpowers(L.r(s + 1), pb);
 #endif
-                    coupling(pb, B);
+                    coupling_p(pb, B);
                 }
                 double b[3], x0, x1, x2;
 #pragma unroll
@@ -1032,14 +1070,18 @@ __device__ __forceinline__ void axis_coeffs(double ws, double we, double r, bool
     const double v1 = right ? -xs[0] : xe[0], a1 = right ? xs[1] : xe[1], j1 = right ? -xs[2] : xe[2];
     const double r2 = r * r, r3 = r2 * r, r4 = r2 * r2;
     const double D = (w1 - w0) * r3;
-    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;
-    const double P4 = 35.0 * D - 20.0 * V0 - 5.0 * A0 - (2.0 / 3.0) * j0 - 15.0 * V1 + 2.5 * A1 - (1.0 / 6.0) * j1;
-    const double P5 = -84.0 * D + 45.0 * V0 + 10.0 * A0 + j0 + 39.0 * V1 - 7.0 * A1 + 0.5 * j1;
-    const double P6 = 70.0 * D - 36.0 * V0 - 7.5 * A0 - (2.0 / 3.0) * j0 - 34.0 * V1 + 6.5 * A1 - 0.5 * j1;
-    const double P7 = -20.0 * D + 10.0 * V0 + 2.0 * A0 + (1.0 / 6.0) * j0 + 10.0 * V1 - 2.0 * A1 + (1.0 / 6.0) * j1;
+    const double V0 = v0 * r2, A0 = a0 * r, V1 = v1 * r2, A1 = a1 * r;  // scaled: x PSV, x PSA
+    const double P4 = 35.0 * D - (20.0 * PSV) * V0 - (5.0 * PSA) * A0 - (2.0 / 3.0) * j0 - (15.0 * PSV) * V1 +
+                      (2.5 * PSA) * A1 - (1.0 / 6.0) * j1;
+    const double P5 = -84.0 * D + (45.0 * PSV) * V0 + (10.0 * PSA) * A0 + j0 + (39.0 * PSV) * V1 -
+                      (7.0 * PSA) * A1 + 0.5 * j1;
+    const double P6 = 70.0 * D - (36.0 * PSV) * V0 - (7.5 * PSA) * A0 - (2.0 / 3.0) * j0 - (34.0 * PSV) * V1 +
+                      (6.5 * PSA) * A1 - 0.5 * j1;
+    const double P7 = -20.0 * D + (10.0 * PSV) * V0 + (2.0 * PSA) * A0 + (1.0 / 6.0) * j0 + (10.0 * PSV) * V1 -
+                      (2.0 * PSA) * A1 + (1.0 / 6.0) * j1;
     c[0] = w0;
-    c[1] = v0;
-    c[2] = 0.5 * a0;
+    c[1] = PSV * v0;
+    c[2] = (0.5 * PSA) * a0;
     c[3] = j0 * (1.0 / 6.0);
     c[4] = P4 * r;
     c[5] = P5 * r2;
@@ -1077,7 +1119,7 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
         for (int d = 0; d < 3; ++d) {
             const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
             const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
-            u0[a][d] = right ? ((d == 1) ? s1 : -s1) : s0;
+            u0[a][d] = (right ? ((d == 1) ? s1 : -s1) : s0) * PSI[d];  // scaled unknowns
         }
     // ---- forward substitution, three axes per knot ----
     double Y[NS + 1][3][3];  // [knot][axis][derivative]
@@ -1108,7 +1150,7 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
             rpowers(L.r(k), pn);
 #endif
             double B[3][3];
-            if (s >= 1) coupling(pp, B);
+            if (s >= 1) coupling_p(pp, B);
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 double y[3];
@@ -1148,7 +1190,7 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
         {
             double pc[8];
             rpowers(L.r(nl), pc);
-            coupling(pc, Cc);
+            coupling_p(pc, Cc);
         }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -1218,7 +1260,7 @@ __device__ __forceinline__ int32_t pair_solve_joint(const LaneView& L, bool righ
 #else
                 rpowers(L.r(s + 1), pb);
 #endif
-                coupling(pb, B);
+                coupling_p(pb, B);
             }
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -1318,8 +1360,8 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
                 const double s0 = (HAS_ED && valid) ? ed[d * 3 + a] : 0.0;
                 const double s1 = (HAS_ED && valid) ? ed[9 + d * 3 + a] : 0.0;
                 const double f = (d == 1) ? 1.0 : sg;
-                u0[d][a] = right ? f * s1 : s0;
-                uM[d][a] = right ? f * s0 : s1;
+                u0[d][a] = (right ? f * s1 : s0) * PSI[d];  // scaled unknowns
+                uM[d][a] = (right ? f * s0 : s1) * PSI[d];
             }
         bool spd = true;
         double fin = 0.0;
@@ -1330,11 +1372,11 @@ __device__ __forceinline__ int32_t pair_solve(const LaneView& L, bool right, V&&
             double pp[8], pn[8], y[3][3], x[3][3];
             rpowers(L.r(0), pp);
             rpowers(L.r(1), pn);
-            const Sym3 D = knot_diag(pp, pn);
+            const Sym3 D = knot_diag_p(pp, pn);
             knot_rhs<HAS_ED>(L, 1, pp, pn, u0, y);
             if (HAS_ED) {  // final derivatives through C_1 (virtual segment 1)
                 double C1[3][3];
-                coupling(pn, C1);
+                coupling_p(pn, C1);
 #pragma unroll
                 for (int d = 0; d < 3; ++d)
 #pragma unroll
@@ -1568,6 +1610,34 @@ __global__ __launch_bounds__(64, TGMS_WAVES(M)) void k_reduced_uniform(int32_t B
 //   g_i = dJ_i/dT_i + k_T,   T_i <- T_i exp(clamp(-eta T_i g_i / F, -1/2, 1/2)),
 // (the clamp bounds one step to a factor e^(+-1/2); trajectories whose solve failed
 // keep their times).  oracle_refine_times restates the same step on the CPU.
+//
+// exp of the clamped step (|x| <= 1/2) as one degree-12 polynomial, Horner with FMAs: the
+// library exp's range reduction, ldexp and overflow selects (~28 VALU per segment) are dead
+// weight on this range.  Coefficients: Chebyshev interpolation at 60 digits
+// (scripts/exp_poly.py), worst error 0.83 ulp over [-1/2, 1/2] with every FMA rounded.
+// TGMS_EXP_LIBM=1 keeps the library exp (A/B builds).
+#ifndef TGMS_EXP_LIBM
+#define TGMS_EXP_LIBM 0
+#endif
+__device__ __forceinline__ double exp_step(double x) {
+#if TGMS_EXP_LIBM
+    return exp(x);
+#else
+    double p = 2.0970151215169475e-09;
+    p = fma(p, x, 2.5182899238184787e-08);
+    p = fma(p, x, 2.7557027169443954e-07);
+    p = fma(p, x, 2.755691018636409e-06);
+    p = fma(p, x, 2.480158773980975e-05);
+    p = fma(p, x, 0.00019841270455051358);
+    p = fma(p, x, 0.0013888888888569297);
+    p = fma(p, x, 0.008333333332885695);
+    p = fma(p, x, 0.041666666666667664);
+    p = fma(p, x, 0.16666666666668065);
+    p = fma(p, x, 0.5);
+    p = fma(p, x, 0.9999999999999999);
+    return fma(p, x, 1.0);
+#endif
+}
 template <int M>
 __device__ __forceinline__ void refine_update(const GradAcc<Chain<M>::NE>& G, bool right, int32_t st, bool live,
                                               double kT, double eta, const double* __restrict__ Tin,
@@ -1593,7 +1663,7 @@ __device__ __forceinline__ void refine_update(const GradAcc<Chain<M>::NE>& G, bo
             const int phys = right ? M - 1 - e : e;
             double dtau = -eta * Tl[e] * (G.dJ[e] + kT) * iF;
             dtau = fmin(fmax(dtau, -0.5), 0.5);
-            Tout[phys] = ok ? Tl[e] * exp(dtau) : Tl[e];
+            Tout[phys] = ok ? Tl[e] * exp_step(dtau) : Tl[e];
         }
     }
     if (live && !right && cost) *cost = F;
@@ -1807,7 +1877,7 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
                 const double tl = Tl[e];
                 double dtau = -eta * tl * (G.dJ[e] + kT) * iF;
                 dtau = fmin(fmax(dtau, -0.5), 0.5);
-                const double tn = ok ? tl * exp(dtau) : tl;
+                const double tn = ok ? tl * exp_step(dtau) : tl;
                 Tl[e] = tn;
                 sm.in.R[r_at<M>(phys, slot)] = fast_rcp(tn);
             }
