@@ -604,6 +604,94 @@ def host_line(solver, B, M, W, T, reps=20):
                     "calls; median of the calls"}
 
 
+def config2_line(solver, dev, stream, reps=200, B=1024, M=3):
+    """Config 2 (BASELINE configs[1]): a batch of 1,024 random 4-waypoint goals (M = 3), fp64,
+    one MI355X.  1,024 trajectories are 32 lane-pair wavefronts: the call is launch- and
+    latency-bound, not HBM-bound, so this line reports times, not a roofline:
+      - `device_us`: HIP events over `reps` back-to-back launches on device buffers;
+      - `sync_call_us`: one launch + stream synchronise, median wall clock per call;
+      - `host_call_us`: tgms_solve_batch on host buffers (H2D, solve, D2H), median;
+      - the literal KKT methods on the same batch (band LU, dense Gauss-Jordan), events;
+      - the CPU oracle on the same batch, reduced formulation and dense KKT, one core;
+    and the GPU coefficients of every method against the oracle's (norm-wise per
+    (trajectory, axis), outside every timed region)."""
+    import torch
+    from oracle import oracle as O
+    from trajectory_generator_ros2_amd import METHOD_BAND_KKT, METHOD_DENSE_KKT, METHOD_REDUCED
+    from trajectory_generator_ros2_amd import synthetic as S
+    so, W, T = S.uniform_batch(B, M)
+    W2, T2 = np.ascontiguousarray(W.reshape(-1, 3)), np.ascontiguousarray(T.reshape(-1))
+    dW, dT = torch.from_numpy(W2).to(dev), torch.from_numpy(T2).to(dev)
+    dC = torch.empty((B, M, 3, 8), dtype=torch.float64, device=dev)
+    dS = torch.zeros((B,), dtype=torch.int32, device=dev)
+    sp = stream.cuda_stream
+    O.build()
+    R, st = O.solve_batch(so, W2, T2, None, O.KKT_C4, 1)
+    assert (st == 0).all()
+    R = R.reshape(B, M, 3, 8)
+    den = np.abs(R).max(axis=(1, 3))
+    den = np.where(den == 0.0, 1.0, den)
+
+    def err_vs_oracle():
+        G = dC.cpu().numpy()
+        return float((np.abs(G - R).max(axis=(1, 3)) / den).max())
+
+    def events(n):
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(n):
+            solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        assert int((dS != 0).sum().item()) == 0, "solver reported failures"
+        return e0.elapsed_time(e1) / n * 1e3
+
+    methods = {}
+    for name, meth, n in (("band_kkt", METHOD_BAND_KKT, 50), ("dense_kkt", METHOD_DENSE_KKT, 50),
+                          ("reduced", METHOD_REDUCED, reps)):  # reduced last: the handle's method after
+        solver.set_method(meth)
+        dC.fill_(float("nan"))
+        us = events(n)
+        methods[name] = {"device_us": us, "trajectories_per_s": B / (us * 1e-6), "max_rel_err_vs_oracle": err_vs_oracle()}
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        solver.solve_uniform_device(B, M, dW, dT, dC, dS, stream=sp)
+        stream.synchronize()
+        ts.append(time.perf_counter() - t0)
+    sync_us = sorted(ts)[len(ts) // 2] * 1e6
+    out = (np.zeros((B * M, 3, 8)), np.zeros(B, dtype=np.int32))
+    for _ in range(3):
+        solver.solve(so, W2, T2, out=out)
+    th = []
+    for _ in range(50):
+        t0 = time.perf_counter()
+        C, st, worst = solver.solve(so, W2, T2, out=out)
+        th.append(time.perf_counter() - t0)
+    assert worst == 0, worst
+    host_us = sorted(th)[len(th) // 2] * 1e6
+    host_err = float((np.abs(C.reshape(B, M, 3, 8) - R).max(axis=(1, 3)) / den).max())
+
+    def cpu(form):
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 0.3:
+            O.solve_batch(so, W2, T2, None, form, 1)
+            n += 1
+        return (time.perf_counter() - t0) / n * 1e6
+
+    cpu_red, cpu_kkt = cpu(O.REDUCED), cpu(O.KKT_C4)
+    worst_err = max([m["max_rel_err_vs_oracle"] for m in methods.values()] + [host_err])
+    return {"workload": f"config2: {B} random 4-waypoint goals (M = {M}), fp64, rest-to-rest, one MI355X",
+            "device_us": methods["reduced"]["device_us"], "sync_call_us": sync_us, "host_call_us": host_us,
+            "trajectories_per_s": methods["reduced"]["trajectories_per_s"],
+            "methods": methods,
+            "cpu_oracle_1core_us": {"reduced": cpu_red, "dense_kkt": cpu_kkt},
+            "max_rel_err_vs_oracle": worst_err, "tol": 1e-9, "verified": bool(worst_err <= 1e-9),
+            "timing": f"events over {reps} launches (literal methods: 50); sync and host calls: median wall clock"}
+
+
 def sampler_line(solver, n, M, W, T, dC, dev, stream, dt=0.01, reps=5):
     """Sampler on the first n solved trajectories at 100 Hz:
     Goal-layout p/v/a/j/psi/dpsi, HBM-bound by its output."""
@@ -947,6 +1035,8 @@ def main():
                     help="steps of the dense-KKT side line (0: skip).  The dense KKT is a cross-check method "
                          "(DESIGN.md section 4): one timing")
     ap.add_argument("--band-steps", type=int, default=5, help="steps of the band-KKT side line (0: skip)")
+    ap.add_argument("--config2", type=int, default=1,
+                    help="config-2 side line (1,024 x M = 3: every method's latency, host path, CPU oracle): 1/0")
     ap.add_argument("--sample-traj", type=int, default=4096,
                     help="trajectories of the sampler side line at dt = 0.01 (0: skip)")
     ap.add_argument("--config5", type=int, default=1,
@@ -1197,6 +1287,11 @@ def main():
         if args.config5:
             config5_full = full.get("config5_full", full)
 
+    config2 = None
+    if args.config2 and args.method == "reduced" and rank == 0:
+        config2 = _side("config2", lambda: config2_line(solver, dev, stream))
+        solver.set_method(METHOD_REDUCED)
+
     sampler = None
     if args.sample_traj > 0:
         sampler = sampler_line(solver, args.sample_traj, M, W, T, dC, dev, stream)
@@ -1298,6 +1393,7 @@ def main():
             "cache_resident": cache_res,
             "dense_kkt": dense,
             "band_kkt": band,
+            "config2": config2,
             "sampler": sampler,
             "config4": config4,
             "config4_full": config4_full,

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-streams}; mkdir -p $O
-SIDE="--dense-steps 0 --band-steps 0 --sample-traj 0 --config5 0 --config4 0 --cache-resident 0 --host-line 0 --node-line 0 --uniform-large-m 0 --cpu-seconds 0"
+SIDE="--dense-steps 0 --band-steps 0 --sample-traj 0 --config5 0 --config4 0 --cache-resident 0 --host-line 0 --node-line 0 --uniform-large-m 0 --config2 0 --cpu-seconds 0"
 for s in 4 2 1 4 2 1; do
   timeout -k 10 200 python bench.py --steps 50 --warmup 5 --streams $s $SIDE >> $O/ab_streams.jsonl 2>> $O/ab.err || exit 1
 done
