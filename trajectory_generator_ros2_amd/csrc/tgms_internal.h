@@ -100,13 +100,19 @@ struct DevPlan {
     int32_t starts[17];  // starts[m]: first index of group m in the permutation (m = 1..16)
     int32_t so_base;     // so[0]
     int32_t bad;
+    // waves[1] > 0: the refinement loop's one-wave class runs as that many PERSISTENT
+    // wavefronts (round 6, k_refine_loop_dev), each taking the class's tiles from the counter
+    // next[1] (longest groups first) until none is left; 0: one block per tile (always for
+    // the two-wave class, and for a one-wave class with no more tiles than SIMDs)
+    int32_t waves[2];
+    int32_t next[2];
 };
 // Grid of one class's loop launch: every wavefront a group table can hold, whatever the
 // offsets (the blocks beyond the class's last group return at once).
 inline unsigned dev_loop_grid(int32_t n) { return (unsigned)((n + RAGGED_TPW - 1) / RAGGED_TPW + 16); }
 hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int has_ed, int32_t* hist, int32_t* perm,
                                  DevPlan* plan, int32_t* status, double* C, double* cost, hipStream_t stream);
-hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+hipError_t launch_refine_loop_dev(int cls, int32_t n, DevPlan* plan, const int32_t* so, const double* W,
                                   double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
                                   double* C, int32_t* status, hipStream_t stream);
 // The ragged solve of one occupancy class from a device plan (k_reduced_multi's blocks).

@@ -37,6 +37,18 @@ namespace {
 // Waves per SIMD the register allocation must allow: two for the axis-sequential
 // solve while its state fits 256 registers without spilling (M <= 11), else one.
 #define TGMS_WAVES(M) ((M) <= TGMS_TWO_WAVE_MAX_M ? 2 : 1)
+// The refinement loop's one-wave class as persistent waves sized from the plan (round 6,
+// k_refine_loop_dev); TGMS_C5_W1: SIMD time per unit of work of a one-wave tile against a
+// two-wave tile (x 100), TGMS_C5_BIAS: the share's bias (%)
+#ifndef TGMS_C5_PERSIST
+#define TGMS_C5_PERSIST 1
+#endif
+#ifndef TGMS_C5_W1
+#define TGMS_C5_W1 157
+#endif
+#ifndef TGMS_C5_BIAS
+#define TGMS_C5_BIAS 110
+#endif
 // One-wave-per-SIMD kernels solve the three axes side by side (pair_solve_joint).
 // The axis-sequential lane-pair solve reads the next knot's waypoints and 1/T from the
 // LDS stage one step ahead (the per-step SCHED_FENCE otherwise exposes the LDS latency at
@@ -1802,7 +1814,7 @@ __device__ __forceinline__ void reduced_ragged_block(Stage<M>& sm, int64_t blk, 
 // stay in the LDS stage between steps (and in the lanes that own them), and T is read
 // once and written once (in place).  Step for step the same arithmetic as
 // refine_ragged_block + refine_update + reduced_ragged_block.
-template <int M, bool HAS_ED>
+template <int M, bool HAS_ED, bool OPQ = false>
 __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int32_t n,
                                                   const int32_t* __restrict__ perm,
                                                   const int32_t* __restrict__ seg_offsets,
@@ -1813,7 +1825,11 @@ __device__ __forceinline__ void refine_loop_block(Stage<M>& sm, int64_t blk, int
     using CH = Chain<M>;
     constexpr int NE = CH::NE;
     constexpr int NW = (M + 1) * 3;
-    const int lane = threadIdx.x;
+    // OPQ (the one-wave class, whose kernel holds the persistent tile loop): an opaque copy
+    // of the lane index, else every lane-derived LDS offset would be hoisted out of the
+    // loop and held over it (~100 of them: 372-636 B of scratch at M = 14..16)
+    int lane = threadIdx.x;
+    if constexpr (OPQ) asm volatile("" : "+v"(lane));
     const int slot = lane >> 1;
     const bool right = lane & 1;
     const int64_t i0 = blk * TPW;
@@ -2007,11 +2023,50 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_multi(GroupTable
     }
 }
 
-// The refinement loop with the device-computed plan (k_plan_scatter): the class's group
-// table is read from device memory (scalar loads), the grid covers every wavefront a
-// table can hold (dev_loop_grid) and the blocks past the class's last group return.
+// One wavefront tile of the refinement loop from the device plan: the class's group table
+// is read from device memory (scalar loads); the tile's group gives M.
 template <int MLO, int MHI, bool HAS_ED>
-__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_dev(const DevPlan* __restrict__ plan, int cls,
+__device__ __forceinline__ void refine_loop_tile(unsigned char* raw, const GroupTable& tab, int64_t tile,
+                                                 const int32_t* __restrict__ seg_offsets,
+                                                 const double* __restrict__ W, double* __restrict__ T,
+                                                 const double* __restrict__ ED, double kT, double eta, int32_t iters,
+                                                 double* __restrict__ cost, double* __restrict__ C,
+                                                 int32_t* __restrict__ status, int32_t so_base) {
+    int64_t blk;
+    const int g = group_of(tab, tile, blk);
+    switch (tab.m[g]) {
+#define TGMS_MULTI_CASE(mm)                                                                                    \
+    case mm:                                                                                                  \
+        if constexpr (mm >= MLO && mm <= MHI)                                                                 \
+            refine_loop_block<mm, HAS_ED, TGMS_WAVES(MHI) == 1>(*reinterpret_cast<Stage<mm>*>(raw), blk,       \
+                                                                 tab.n[g], tab.perm[g], seg_offsets, W, T, ED, kT, \
+                                                                 eta, iters, cost, C, status, so_base);            \
+        break;
+        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
+        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
+        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
+        TGMS_MULTI_CASE(16)
+#undef TGMS_MULTI_CASE
+        default: break;
+    }
+}
+
+// The refinement loop from the device plan, one launch per occupancy class, in one of two
+// modes the plan chooses (k_plan_scatter):
+//   * plan->waves[cls] == 0: one block per wavefront tile (longest groups first), blocks
+//     past the class's last tile return; the hardware dispatches tiles into free slots;
+//   * plan->waves[cls] > 0 (the one-wave class when it has more tiles than the GPU has
+//     SIMDs, TGMS_C5_PERSIST): that many PERSISTENT wavefronts, each holding its SIMD and
+//     taking tiles from plan->next[cls] (zeroed by the planner) until none is left.  A
+//     one-wave tile needs a whole SIMD, which a SIMD shared with the two-wave class never
+//     frees while two-wave tiles are pending: at full config-5 size (6,563 one-wave tiles)
+//     the class was starved while the two-wave class ran and then ran alone as the tail;
+//     sized from the plan's per-class work, the persistent class ends with the other one
+//     (1,048,576 ragged on one device: 2.52-2.53 -> 2.35-2.37 ms pipelined, session r06v).
+//     At one shard (822 tiles: one round) one block per tile is as fast (r06v, r06x).
+// Which wave takes which tile does not change a tile's arithmetic: results are bit-identical.
+template <int MLO, int MHI, bool HAS_ED>
+__global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_dev(DevPlan* __restrict__ plan, int cls,
                                                                           const int32_t* __restrict__ seg_offsets,
                                                                           const double* __restrict__ W,
                                                                           double* __restrict__ T,
@@ -2023,23 +2078,29 @@ __global__ __launch_bounds__(64, TGMS_WAVES(MHI)) void k_refine_loop_dev(const D
     __shared__ alignas(16) unsigned char raw[max_stage_bytes<MLO, MHI>()];
     const GroupTable& tab = plan->tab[cls];
     const int ng = tab.ngroups;
-    if (ng <= 0 || (int64_t)blockIdx.x >= tab.blk_end[ng - 1]) return;
-    int64_t blk;
-    const int g = group_of(tab, blockIdx.x, blk);
+    if (ng <= 0) return;
+    const int64_t ntiles = tab.blk_end[ng - 1];
     const int32_t so_base = plan->so_base;
-    switch (tab.m[g]) {
-#define TGMS_MULTI_CASE(mm)                                                                                    \
-    case mm:                                                                                                  \
-        if constexpr (mm >= MLO && mm <= MHI)                                                                 \
-            refine_loop_block<mm, HAS_ED>(*reinterpret_cast<Stage<mm>*>(raw), blk, tab.n[g], tab.perm[g],     \
-                                          seg_offsets, W, T, ED, kT, eta, iters, cost, C, status, so_base);  \
-        break;
-        TGMS_MULTI_CASE(1) TGMS_MULTI_CASE(2) TGMS_MULTI_CASE(3) TGMS_MULTI_CASE(4) TGMS_MULTI_CASE(5)
-        TGMS_MULTI_CASE(6) TGMS_MULTI_CASE(7) TGMS_MULTI_CASE(8) TGMS_MULTI_CASE(9) TGMS_MULTI_CASE(10)
-        TGMS_MULTI_CASE(11) TGMS_MULTI_CASE(12) TGMS_MULTI_CASE(13) TGMS_MULTI_CASE(14) TGMS_MULTI_CASE(15)
-        TGMS_MULTI_CASE(16)
-#undef TGMS_MULTI_CASE
-        default: break;
+    // (the persistent loop is compiled into the one-wave class only: at two waves per SIMD
+    // its live ranges would not fit the 256 registers)
+    const int nw = TGMS_WAVES(MHI) == 1 ? plan->waves[cls] : 0;
+    if (nw <= 0) {
+        if ((int64_t)blockIdx.x >= ntiles) return;
+        refine_loop_tile<MLO, MHI, HAS_ED>(raw, tab, blockIdx.x, seg_offsets, W, T, ED, kT, eta, iters, cost, C,
+                                           status, so_base);
+        return;
+    }
+    if constexpr (TGMS_WAVES(MHI) == 1) {
+        if ((int)blockIdx.x >= nw) return;
+        for (;;) {
+            int tile = 0;
+            if (threadIdx.x == 0) tile = atomicAdd(&plan->next[cls], 1);  // a vector atomic, one lane
+            tile = __builtin_amdgcn_readfirstlane(tile);
+            if ((int64_t)tile >= ntiles) break;  // every wave leaves once the tiles run out
+            refine_loop_tile<MLO, MHI, HAS_ED>(raw, tab, tile, seg_offsets, W, T, ED, kT, eta, iters, cost, C, status,
+                                               so_base);
+            __syncthreads();  // the next tile re-stages the LDS
+        }
     }
 }
 
@@ -2165,7 +2226,7 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_perm_scatter(int32_t B, const in
 // TGMS_ERR_SKIPPED, all outputs exact zeros (each block its own trajectories and its share
 // of the S x 24 coefficients).
 __global__ __launch_bounds__(PERM_BLOCK) void k_plan_scatter(int32_t n, int64_t S, const int32_t* __restrict__ so,
-                                                             int has_ed, const int32_t* __restrict__ hist,
+                                                             int has_ed, int nsimd, const int32_t* __restrict__ hist,
                                                              int32_t* __restrict__ perm, DevPlan* __restrict__ plan,
                                                              int32_t* __restrict__ status, double* __restrict__ C,
                                                              double* __restrict__ cost) {
@@ -2236,6 +2297,36 @@ __global__ __launch_bounds__(PERM_BLOCK) void k_plan_scatter(int32_t n, int64_t 
             }
             plan->tab[0].ngroups = ng[0];
             plan->tab[1].ngroups = ng[1];
+            // the one-wave class's persistent waves (k_refine_loop_dev): its share of the
+            // machine's SIMD time from the per-class work (tiles x (2 + M), the host
+            // planner's cost), a one-wave tile taking TGMS_C5_W1 / 100 times the SIMD time
+            // of a two-wave tile per unit (session r06r: 122 us per one-wave tile at M ~ 15
+            // holding a SIMD, 87 us per two-wave tile at M ~ 7.5 sharing one), biased up by
+            // TGMS_C5_BIAS % so the coarse class ends before the fine one, not after
+            plan->next[0] = 0;
+            plan->next[1] = 0;
+            plan->waves[0] = 0;
+            plan->waves[1] = 0;
+            if (TGMS_C5_PERSIST && !bad) {
+                int64_t w1 = 0, w2 = 0, t1 = 0;
+                for (int k = 1; k < PERM_BINS; ++k) {
+                    const int64_t tiles = (cnt[k] + RAGGED_TPW - 1) / RAGGED_TPW;
+                    if (k > max2) {
+                        w1 += tiles * (2 + k) * TGMS_C5_W1;
+                        t1 += tiles;
+                    } else {
+                        w2 += tiles * (2 + k) * 100;
+                    }
+                }
+                if (t1 > 0) {
+                    int64_t p = ((int64_t)nsimd * w1 * TGMS_C5_BIAS + (w1 + w2) * 100 - 1) / ((w1 + w2) * 100);
+                    p = p < 1 ? 1 : p;
+                    p = p > nsimd ? nsimd : p;
+                    // persistent only when the class has more tiles than the GPU has SIMDs
+                    // (one block per tile then needs every one of them: grid <= nsimd)
+                    plan->waves[1] = t1 > nsimd ? (int32_t)p : 0;
+                }
+            }
         }
     }
     __syncthreads();
@@ -3110,30 +3201,48 @@ hipError_t launch_group_perm(int32_t B, const int32_t* so, const int32_t* starts
     return hipSuccess;
 }
 
+// SIMDs of the current device (4 per CU), cached per device
+int device_simds() {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+    if (cache[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return 1024;
+        cache[dev] = 4 * cus;
+    }
+    return cache[dev];
+}
+
 hipError_t launch_group_plan_dev(int32_t n, int64_t S, const int32_t* so, int has_ed, int32_t* hist, int32_t* perm,
                                  DevPlan* plan, int32_t* status, double* C, double* cost, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + PERM_BLOCK - 1) / PERM_BLOCK);
     TGMS_LAUNCH(k_perm_hist, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, so, hist);
-    TGMS_LAUNCH(k_plan_scatter, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, S, so, has_ed, hist, perm, plan, status,
-                C, cost);
+    TGMS_LAUNCH(k_plan_scatter, dim3(grid), dim3(PERM_BLOCK), 0, stream, n, S, so, has_ed, device_simds(), hist, perm,
+                plan, status, C, cost);
     return hipSuccess;
 }
 
 // (instantiated only for the classes a call can launch: end derivatives use the ED
 // boundary, so e.g. <1, TWO_WAVE_MAX_M, true> never exists)
 template <int MLO, int MHI, bool HAS_ED>
-hipError_t loop_dev_launch(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W, double* T,
+hipError_t loop_dev_launch(int cls, int32_t n, DevPlan* plan, const int32_t* so, const double* W, double* T,
                            const double* ED, double kT, double eta, int32_t iters, double* cost, double* C,
                            int32_t* status, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
+    // the one-wave class: as many blocks as SIMDs at most (persistent when it has more tiles
+    // than that, k_plan_scatter); the two-wave class one block per tile
+    unsigned grid = dev_loop_grid(n);
+    if (TGMS_C5_PERSIST && cls == 1) grid = std::min<unsigned>(grid, (unsigned)device_simds());
     if constexpr (MLO <= MHI)  // (MLO > MHI: an empty class, every M at two waves)
-        TGMS_LAUNCH((k_refine_loop_dev<MLO, MHI, HAS_ED>), dim3(dev_loop_grid(n)), dim3(W64), 0, stream, plan, cls,
-                    so, W, T, ED, kT, eta, iters, cost, C, status);
+        TGMS_LAUNCH((k_refine_loop_dev<MLO, MHI, HAS_ED>), dim3(grid), dim3(W64), 0, stream, plan, cls, so, W, T, ED,
+                    kT, eta, iters, cost, C, status);
     return hipSuccess;
 }
 
-hipError_t launch_refine_loop_dev(int cls, int32_t n, const DevPlan* plan, const int32_t* so, const double* W,
+hipError_t launch_refine_loop_dev(int cls, int32_t n, DevPlan* plan, const int32_t* so, const double* W,
                                   double* T, const double* ED, double kT, double eta, int32_t iters, double* cost,
                                   double* C, int32_t* status, hipStream_t stream) {
     constexpr int A = TGMS_TWO_WAVE_MAX_M, E = TGMS_TWO_WAVE_MAX_M_ED;
