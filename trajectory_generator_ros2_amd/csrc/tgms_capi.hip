@@ -676,14 +676,23 @@ tgms_status solve_ragged_dev(tgms_handle* h, int32_t B, int64_t S, const int32_t
 // caller): one load per trajectory against an induction variable, in blocks of 4,096 that
 // stop at the first block holding a different M.  Modulo 2^32 is exact here: offsets in
 // [0, 2^31) congruent to M0 b for every b step by exactly M0.
-bool uniform_offsets(int32_t B, const int32_t* so, int32_t M0) {
-    const uint32_t m = (uint32_t)M0;
-    uint32_t diff = 0;
-    for (int32_t b0 = 0; b0 <= B && diff == 0; b0 += 4096) {
-        const int32_t e = std::min(B + 1, b0 + 4096);
-        for (int32_t b = b0; b < e; ++b) diff |= (uint32_t)so[b] ^ (m * (uint32_t)b);
-    }
+// (built for AVX2 where the CPU has it, as minmax_m above: the inner loop vectorises)
+#define TGMS_UNIFORM_BODY                                                                 \
+    const uint32_t m = (uint32_t)M0;                                                      \
+    uint32_t diff = 0;                                                                    \
+    for (int32_t b0 = 0; b0 <= B && diff == 0; b0 += 4096) {                              \
+        const int32_t e = std::min(B + 1, b0 + 4096);                                     \
+        for (int32_t b = b0; b < e; ++b) diff |= (uint32_t)so[b] ^ (m * (uint32_t)b);     \
+    }                                                                                     \
     return diff == 0;
+__attribute__((target("avx2"))) bool uniform_offsets_avx2(int32_t B, const int32_t* so, int32_t M0) {
+    TGMS_UNIFORM_BODY
+}
+bool uniform_offsets_base(int32_t B, const int32_t* so, int32_t M0) { TGMS_UNIFORM_BODY }
+#undef TGMS_UNIFORM_BODY
+bool uniform_offsets(int32_t B, const int32_t* so, int32_t M0) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    return avx2 ? uniform_offsets_avx2(B, so, M0) : uniform_offsets_base(B, so, M0);
 }
 
 // The host check of a multi-GPU ragged solve with the reduced method (round 6, as the
